@@ -1,0 +1,231 @@
+/*
+ * packos.h — C ABI of the MI355X-native bulk PackOS encoder/decoder.
+ *
+ * One call encodes (or decodes) a whole batch of independent PackOS blobs that
+ * share one fixed schema.  Everything is plain pointers and sizes: no HIP or
+ * torch types cross this boundary, so a Go cgo shim, a C++
+ * program or Python ctypes can bind it directly.
+ *
+ * Reference interfaces each entry point replaces (quickwritereader/PackOS):
+ *   packos_schema_compile  <- schema.BuildSchema(*SchemaJSON)          schema/schemabuilder_json.go:124
+ *                             + utils.SortKeys resolved once             utils/utils.go:7
+ *   packos_encode_batch    <- access.PutAccess Add..., Pack()  (MODE_PUTACCESS)   access/put.go:69-308,619
+ *                             schema.EncodeValue / EncodeValueNamed (MODE_PUTACCESS) schema/schema.go:912,968
+ *                             packable.Pack(args...)        (MODE_PACKABLE)    packable/pack.go:59
+ *   packos_encoded_size_batch <- PutAccess.PackSize / Tuple.ValueSize      access/put.go:655, packable/pack.go:17
+ *   packos_decode_batch    <- schema.DecodeBuffer / DecodeBufferNamed / ValidateBuffer
+ *                             over access.SeqGetAccess                  schema/schema.go:880,893,948; access/seqget.go
+ *   packos_get_field_batch <- access.GetAccess Get*(pos) / GetNestedGetAccess  access/get.go:19-375,492
+ *   packos_strerror        <- Go error strings (errors.New / SchemaError.Error)
+ *
+ * Conventions
+ *   - All data pointers passed to the batch calls are DEVICE pointers (hipMalloc
+ *     or torch CUDA tensors) unless stated otherwise; the caller owns every
+ *     buffer.  Calls are asynchronous on the given stream (a hipStream_t passed
+ *     as void*, NULL = default stream).
+ *   - Return value: 0 on success, a negative PACKOS_E* code otherwise.  Per-blob
+ *     outcomes go to the `status` array (see PACKOS_STATUS_ macros).
+ *   - A compiled schema handle is immutable and may be shared across threads and
+ *     devices.
+ */
+#ifndef PACKOS_H
+#define PACKOS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PACKOS_ABI_VERSION 1
+
+/* ---- return codes (library-level errors) -------------------------------- */
+#define PACKOS_OK              0
+#define PACKOS_E_INVALID      -1   /* bad argument */
+#define PACKOS_E_SCHEMA       -2   /* schema JSON rejected (message via packos_last_error) */
+#define PACKOS_E_UNSUPPORTED  -3   /* schema feature outside the compiled subset */
+#define PACKOS_E_ALIGN        -4   /* a fixed-width column is not 16-byte aligned */
+#define PACKOS_E_WORKSPACE    -5   /* workspace too small */
+#define PACKOS_E_CAPACITY     -6   /* output arena smaller than the encoded batch */
+#define PACKOS_E_HIP          -7   /* HIP runtime error (message via packos_last_error) */
+#define PACKOS_E_NODEVICE     -8   /* no GPU visible */
+
+/* ---- encode modes --------------------------------------------------------- */
+/* PutAccess.Pack() / schema.EncodeValue bytes: no slack, empty nested
+ * container written by BeginTuple/EndNested is the 2-byte blob 10 00.         */
+#define PACKOS_MODE_PUTACCESS  0
+/* packable.Pack(args...) bytes: buffer sized by ValueSize(), so every nil
+ * nullable leaves its full width as zero slack after the End-marked payload
+ * (access/direct_write_nullables.go:10-12, packable/packable_nullables.go:23);
+ * PackTuple() with no args writes nothing (packable/pack.go:31).             */
+#define PACKOS_MODE_PACKABLE   1
+
+/* ---- PackOS type tags (typetags/types.go:6-20) ---------------------------- */
+#define PACKOS_TAG_END      0
+#define PACKOS_TAG_INTEGER  1
+#define PACKOS_TAG_EXTENDED 2
+#define PACKOS_TAG_FLOATING 3
+#define PACKOS_TAG_TUPLE    4
+#define PACKOS_TAG_BOOL     5
+#define PACKOS_TAG_STRING   6
+#define PACKOS_TAG_MAP      7
+
+/* ---- leaf (column) kinds -------------------------------------------------- */
+#define PACKOS_KIND_INT     1   /* int8/16/32/64  (tag Integer)  */
+#define PACKOS_KIND_UINT    2   /* uint8/16/32/64 (tag Integer)  */
+#define PACKOS_KIND_FLOAT   3   /* float32/64 raw bits (tag Floating) */
+#define PACKOS_KIND_BOOL    4   /* one byte, any non-zero input encodes as 1 */
+#define PACKOS_KIND_STRING  5   /* tag String */
+#define PACKOS_KIND_BYTES   6   /* tag String (ByteArray) */
+#define PACKOS_KIND_TUPLE   7   /* nested tuple: column carries only `valid` */
+#define PACKOS_KIND_MAP     8   /* nested map:   column carries only `valid` */
+
+/* ---- per-blob status word -------------------------------------------------
+ * bits 0..7   schema ErrorCode of the error DecodeBuffer/ValidateBuffer would
+ *             return (schema/schema.go:24-41); 0 = ok
+ * bits 8..23  top-level field position of that error + 1 (0 = position -1)
+ * bit 30      the reference would panic (Go runtime index out of range) on
+ *             this blob, e.g. a nullable int16 field of width 1
+ * bit 31      encode: an offset >= 8192 was truncated to 13 bits exactly as
+ *             typetags.EncodeHeader does (Q1); the bytes still match the
+ *             reference, the flag only reports it
+ */
+#define PACKOS_STATUS_CODE(s)      ((int)((s) & 0xFFu))
+#define PACKOS_STATUS_POS(s)       ((int)(((s) >> 8) & 0xFFFFu) - 1)
+#define PACKOS_STATUS_PANIC        0x40000000u
+#define PACKOS_STATUS_OVERFLOW13   0x80000000u
+
+/* schema.ErrorCode values (schema/schema.go:24-41) */
+#define PACKOS_ERR_INVALID_FORMAT        1
+#define PACKOS_ERR_UNEXPECTED_EOF        2
+#define PACKOS_ERR_CONSTRAINT_VIOLATED   3
+#define PACKOS_ERR_ENCODE                4
+#define PACKOS_ERR_STRING_MATCH          9
+#define PACKOS_ERR_OUT_OF_RANGE         13
+
+/* ---- columns ---------------------------------------------------------------
+ * One packos_column per schema node in depth-first (pre-order) schema order:
+ * every leaf and every nested tuple/map has a column; map-key literals
+ * ("exact" strings) are compile-time constants and have none.  A tuple/map
+ * column only uses `valid` (nil container = header with zero width, the
+ * AddAnyTuple(nil)/AddMapAny(nil) form, access/put.go:343-352,547-553).
+ *
+ *   fixed-width leaf : data = n*width bytes, row i at data + i*width
+ *                      (16-byte aligned base; little-endian scalars)
+ *   var-width leaf   : encode input: data = byte arena, offsets = n+1 uint32
+ *                      (row i = data[offsets[i] .. offsets[i+1]))
+ *                      decode output: start[i] = absolute arena offset of the
+ *                      payload, length[i] = its width (the payload aliases the
+ *                      input arena, like GetBytes/GetStringUnsafe,
+ *                      access/get.go:335-375)
+ *   nullable leaf    : valid = n bytes, 1 = value present, 0 = nil
+ *                      (encode input; decode output).  NULL on encode = all
+ *                      present.
+ */
+typedef struct packos_column {
+    void*           data;
+    const uint32_t* offsets;
+    uint8_t*        valid;
+    uint64_t*       start;
+    uint32_t*       length;
+} packos_column;
+
+typedef struct packos_column_info {
+    int32_t kind;       /* PACKOS_KIND_* */
+    int32_t width;      /* fixed byte width, 0 = variable */
+    int32_t nullable;   /* 1 = has a validity column */
+    int32_t tag;        /* PACKOS_TAG_* written in its header */
+    int32_t top_index;  /* index of the top-level field this leaf belongs to */
+    int32_t depth;      /* 0 = top-level field */
+    char    name[96];   /* dotted path of fieldNames ("" when unnamed) */
+} packos_column_info;
+
+typedef struct packos_schema packos_schema;
+
+/* ---- schema compiler (host only, no GPU needed) -------------------------- */
+
+/* Compile a schema given in the SchemaJSON vocabulary
+ * (schema/schemabuilder_json.go:8-30).  Accepted top level: a JSON array
+ * (SChain) or {"type":"chain","schema":[...],"fieldNames":[...]}
+ * (SchemaNamedChain).  Supported node types: bool, int8..int64,
+ * uint8..uint64, float32, float64, string (width / nullable / exact),
+ * bytes (width), tuple (schema, fieldNames, nullable, variableLength),
+ * map (schema = key,value,... ; keys with "exact" become constants;
+ * "sorted": true sorts the pairs by key bytes at compile time, which is
+ * PackMapSorted / AddMapSortedKey order).                                    */
+int  packos_schema_compile(const char* schema_json, int mode, packos_schema** out);
+void packos_schema_free(packos_schema* s);
+int  packos_schema_num_columns(const packos_schema* s);
+int  packos_schema_num_top_fields(const packos_schema* s);
+int  packos_schema_column_info(const packos_schema* s, int col, packos_column_info* out);
+/* Blob size in bytes when every blob has the same size, else -1. */
+int64_t packos_schema_fixed_blob_size(const packos_schema* s);
+/* Host-side dump of the compiled layout program (debug/testing). Returns the
+ * number of bytes needed (including NUL); writes at most cap bytes.          */
+size_t packos_schema_describe(const packos_schema* s, char* buf, size_t cap);
+/* Host-side encoded size of one blob given its var widths / valid flags,
+ * without a GPU (used by shard planning).  widths[c] is read for var
+ * columns, valid[c] for nullable columns (may be NULL).                      */
+int64_t packos_schema_blob_size_host(const packos_schema* s, const uint32_t* widths,
+                                     const uint8_t* valid);
+
+/* ---- batch encode ---------------------------------------------------------- */
+
+/* Workspace (device memory) a batch of n blobs needs. */
+size_t packos_encode_workspace_size(const packos_schema* s, size_t n_blobs);
+
+/* Size pass + exclusive scan: out_offsets[0..n] (device, uint64).  Fixed-size
+ * schemas write i*B without reading columns.                                 */
+int packos_encoded_size_batch(const packos_schema* s, const packos_column* cols, size_t n_blobs,
+                              uint64_t* out_offsets, void* workspace, size_t workspace_bytes,
+                              void* stream);
+
+/* Encode n blobs into out_arena.  For a variable-size schema out_offsets
+ * (n+1, device) receives each blob's start; pass flags PACKOS_ENC_OFFSETS_READY
+ * when out_offsets already holds the result of packos_encoded_size_batch to
+ * skip the size pass.  For a fixed-size schema out_offsets may be NULL (blob i
+ * is at i*B).  status (n, device) may be NULL.  out_capacity is checked only
+ * when offsets are known on the host side (fixed schemas); for variable
+ * schemas blobs that would end past out_capacity are not written and get
+ * PACKOS_ERR_ENCODE in their status.                                         */
+#define PACKOS_ENC_OFFSETS_READY 1u
+int packos_encode_batch(const packos_schema* s, const packos_column* cols, size_t n_blobs,
+                        uint8_t* out_arena, uint64_t out_capacity, uint64_t* out_offsets,
+                        uint32_t* status, void* workspace, size_t workspace_bytes,
+                        uint32_t flags, void* stream);
+
+/* ---- batch decode (schema.DecodeBuffer semantics) ------------------------- */
+
+/* blob i = arena[offsets[i] .. offsets[i+1]); offsets == NULL means fixed
+ * stride `stride` bytes.  Every blob is validated with SeqGetAccess/precheck
+ * rules; status[i] gets the error DecodeBuffer would return.  Columns of a
+ * failing blob are left unspecified.                                         */
+int packos_decode_batch(const packos_schema* s, const uint8_t* arena, const uint64_t* offsets,
+                        uint64_t stride, size_t n_blobs, packos_column* out_cols,
+                        uint32_t* status, void* stream);
+
+/* ---- random-access gather (GetAccess semantics) --------------------------- */
+
+/* For each blob walk `depth` positions (GetNestedGetAccess for all but the
+ * last) and read the field at the last position:
+ *   out_start[i]/out_len[i] = absolute [start,end) of the field payload,
+ *   out_tag[i]  = its tag,
+ *   status[i]   = 0 ok, 1 decode error (the Get* call would return an error
+ *                 for `want_tag`/`want_width`), 2 nil nested access.
+ * want_width < 0 accepts any width >= 0 (GetBytes/GetString);
+ * want_width == 0 is not used.                                               */
+int packos_get_field_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
+                           size_t n_blobs, const int32_t* path, int depth, int want_tag,
+                           int want_width, uint64_t* out_start, uint32_t* out_len,
+                           uint8_t* out_tag, uint8_t* status, void* stream);
+
+/* ---- misc ------------------------------------------------------------------ */
+const char* packos_strerror(int code);
+const char* packos_last_error(void);   /* thread-local detail of the last failure */
+int         packos_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PACKOS_H */

@@ -1,0 +1,678 @@
+/*
+ * packos_oracle.c — CPU ORACLE (test infrastructure only; see packos_oracle.h).
+ *
+ * Plain-C restatement of quickwritereader/PackOS (Go).  Each function cites
+ * the reference file:line it follows.  Used only by tests/, smoke() and the
+ * bench cpu_baseline leg; never linked into libpackos.so.
+ */
+#include "packos_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------ */
+/* typetags/types.go:44-50                                                  */
+/* ------------------------------------------------------------------------ */
+uint16_t or_encode_header(int64_t offset, int tag) {
+    /* uint16(offset<<3) | (uint16(typeID) & 0x07): high bits silently lost */
+    return (uint16_t)(((uint64_t)offset << 3) & 0xFFFFu) | (uint16_t)(tag & 7);
+}
+uint16_t or_encode_end(int64_t offset) { return (uint16_t)(((uint64_t)offset << 3) & 0xFFFFu); }
+
+static inline uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+static inline void wr16(uint8_t* p, uint16_t v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); }
+static inline int ovf(int64_t off) { return off >= 8192 || off < 0; }
+
+/* ------------------------------------------------------------------------ */
+/* PutAccess (access/put.go:46-702)                                         */
+/* ------------------------------------------------------------------------ */
+static void grow(uint8_t** b, size_t* cap, size_t need) {
+    if (need <= *cap) return;
+    size_t nc = *cap ? *cap : 256;
+    while (nc < need) nc *= 2;
+    *b = (uint8_t*)realloc(*b, nc);
+    *cap = nc;
+}
+void or_put_init(or_put* p) { memset(p, 0, sizeof(*p)); }
+void or_put_free(or_put* p) { free(p->buf); free(p->offs); memset(p, 0, sizeof(*p)); }
+/* GetPutAccess: buf[:0], offsets[:0], position 0 (put.go:25-31) */
+void or_put_reset(or_put* p) { p->len = 0; p->olen = 0; p->position = 0; p->overflow = 0; }
+
+static void put_hdr(or_put* p, int64_t off, int tag) {
+    grow(&p->offs, &p->ocap, p->olen + 2);
+    if (ovf(off)) p->overflow = 1;
+    wr16(p->offs + p->olen, or_encode_header(off, tag));
+    p->olen += 2;
+}
+/* Add* / AppendTagAndValue (put.go:69-81, 296-301): the header records the
+ * current position, the payload is appended, position = len(buf).          */
+void or_put_add(or_put* p, int tag, const uint8_t* bytes, size_t n) {
+    put_hdr(p, p->position, tag);
+    grow(&p->buf, &p->cap, p->len + n);
+    if (n) memcpy(p->buf + p->len, bytes, n);
+    p->len += n;
+    p->position = (int64_t)p->len;
+}
+/* AddNullable*(nil): header only, position unchanged (put.go:191-292) */
+void or_put_add_nil(or_put* p, int tag) { put_hdr(p, p->position, tag); }
+/* BeginTuple / BeginMap (put.go:687-698) */
+void or_put_begin(or_put* parent, int tag) { put_hdr(parent, parent->position, tag); }
+
+/* PackAppend (put.go:637-652): End, h0 rewrite, headers then payload */
+static void put_pack_append(or_put* p, uint8_t** dst, size_t* dlen, size_t* dcap) {
+    put_hdr(p, p->position, 0); /* EncodeEnd(position) */
+    size_t hsz = p->olen;
+    int tag0 = p->offs[0] & 7;
+    if (ovf((int64_t)hsz)) p->overflow = 1;
+    wr16(p->offs, or_encode_header((int64_t)hsz, tag0));
+    grow(dst, dcap, *dlen + hsz + p->len);
+    memcpy(*dst + *dlen, p->offs, hsz);
+    if (p->len) memcpy(*dst + *dlen + hsz, p->buf, p->len);
+    *dlen += hsz + p->len;
+}
+/* EndNested -> appendAndReleaseNested (put.go:609-615, 700-702) */
+void or_put_end(or_put* parent, or_put* child) {
+    put_pack_append(child, &parent->buf, &parent->len, &parent->cap);
+    if (child->overflow) parent->overflow = 1;
+    parent->position = (int64_t)parent->len;
+}
+size_t or_put_pack_size(const or_put* p) { return p->olen + p->len + 2; } /* put.go:655-658 */
+/* Pack (put.go:619-635) */
+size_t or_put_pack(or_put* p, uint8_t* out) {
+    put_hdr(p, p->position, 0);
+    size_t hsz = p->olen;
+    int tag0 = p->offs[0] & 7;
+    if (ovf((int64_t)hsz)) p->overflow = 1;
+    wr16(p->offs, or_encode_header((int64_t)hsz, tag0));
+    memcpy(out, p->offs, hsz);
+    if (p->len) memcpy(out + hsz, p->buf, p->len);
+    return hsz + p->len;
+}
+
+/* ------------------------------------------------------------------------ */
+/* schema node helpers                                                      */
+/* ------------------------------------------------------------------------ */
+#define NK(s, n) ((s)->nodes[4 * (n)])
+#define NA(s, n) ((s)->nodes[4 * (n) + 1])
+#define NB(s, n) ((s)->nodes[4 * (n) + 2])
+#define NC(s, n) ((s)->nodes[4 * (n) + 3])
+
+static int is_container(int k) { return k == ORN_TUPLE || k == ORN_MAP; }
+static int nchild(const or_schema* s, int n) { return is_container(NK(s, n)) ? NB(s, n) : 0; }
+
+static int prep_rec(or_schema* s, int n) {
+    if (n >= s->n_nodes || n >= 512) return -1;
+    int k = nchild(s, n);
+    int c = n + 1;
+    for (int j = 0; j < k; j++) {
+        int nx = prep_rec(s, c);
+        if (nx < 0) return -1;
+        c = nx;
+    }
+    s->next_sibling[n] = c;
+    return c;
+}
+static int children(const or_schema* s, int n, int* out);
+/* columns are numbered in emission (wire) order: pre-order with sorted map
+ * pairs already in key order                                                */
+static void number_cols(or_schema* s, int n, int* col) {
+    s->col_of_node[n] = NK(s, n) != ORN_MATCH ? (*col)++ : -1;
+    int kids[256];
+    int k = children(s, n, kids);
+    for (int j = 0; j < k; j++) number_cols(s, kids[j], col);
+}
+int or_schema_prepare(or_schema* s) {
+    int col = 0, c = 0;
+    if (s->n_top > 256) return -1;
+    for (int t = 0; t < s->n_top; t++) {
+        s->top_nodes[t] = c;
+        c = prep_rec(s, c);
+        if (c < 0) return -1;
+    }
+    if (c != s->n_nodes) return -1;
+    for (int t = 0; t < s->n_top; t++) number_cols(s, s->top_nodes[t], &col);
+    s->n_cols = col;
+    return 0;
+}
+
+static int leaf_tag(int k) {
+    switch (k) {
+        case ORN_INT: case ORN_UINT: return 1;
+        case ORN_FLOAT: return 3;
+        case ORN_BOOL: return 5;
+        case ORN_STRING: case ORN_BYTES: case ORN_MATCH: return 6;
+        case ORN_TUPLE: return 4;
+        case ORN_MAP: return 7;
+    }
+    return 0;
+}
+
+static const uint8_t* lit_ptr(const or_schema* s, int li, size_t* len) {
+    *len = (size_t)(s->lit_off[li + 1] - s->lit_off[li]);
+    return s->lit + s->lit_off[li];
+}
+
+/* children of a container in emission order; sorted maps order key/value
+ * pairs by key bytes (utils.SortKeys = sort.Strings, utils/utils.go:7-14). */
+static int children(const or_schema* s, int n, int* out) {
+    int k = nchild(s, n), c = n + 1;
+    for (int j = 0; j < k; j++) { out[j] = c; c = s->next_sibling[c]; }
+    if (NK(s, n) == ORN_MAP && NA(s, n)) {
+        int np = k / 2;
+        for (int a = 1; a < np; a++) {  /* insertion sort on pairs */
+            int kk = out[2 * a], vv = out[2 * a + 1];
+            size_t la; const uint8_t* pa = lit_ptr(s, NA(s, kk), &la);
+            int b = a - 1;
+            while (b >= 0) {
+                size_t lb; const uint8_t* pb = lit_ptr(s, NA(s, out[2 * b]), &lb);
+                size_t m = la < lb ? la : lb;
+                int cmp = memcmp(pb, pa, m);
+                if (cmp < 0 || (cmp == 0 && lb <= la)) break;
+                out[2 * b + 2] = out[2 * b]; out[2 * b + 3] = out[2 * b + 1];
+                b--;
+            }
+            out[2 * b + 2] = kk; out[2 * b + 3] = vv;
+        }
+    }
+    return k;
+}
+
+static int col_valid(const packos_column* c, size_t i) { return !c->valid || c->valid[i]; }
+
+/* leaf payload for blob i: pointer + length (nil -> returns 0 with *nil=1) */
+static const uint8_t* leaf_bytes(const or_schema* s, const packos_column* cols, size_t i, int n,
+                                 size_t* len, int* nil, uint8_t* tmp) {
+    int k = NK(s, n);
+    *nil = 0;
+    if (k == ORN_MATCH) return lit_ptr(s, NA(s, n), len);
+    const packos_column* c = &cols[s->col_of_node[n]];
+    if (k == ORN_STRING || k == ORN_BYTES) {
+        if (NA(s, n) > 0) { *len = (size_t)NA(s, n); return (const uint8_t*)c->data + i * (size_t)NA(s, n); }
+        *len = c->offsets[i + 1] - c->offsets[i];
+        return (const uint8_t*)c->data + c->offsets[i];
+    }
+    int w = NA(s, n);
+    *len = (size_t)w;
+    if (NB(s, n) && !col_valid(c, i)) { *nil = 1; return NULL; }
+    const uint8_t* p = (const uint8_t*)c->data + i * (size_t)w;
+    if (k == ORN_BOOL) { tmp[0] = p[0] != 0; return tmp; } /* AddBool writes 0/1 (put.go:179-189) */
+    return p;
+}
+
+/* ------------------------------------------------------------------------ */
+/* schema.EncodeValue through PutAccess (schema/schema.go:912-941,           */
+/* 594-829, 270-326, 416-457, 1636-1680)                                     */
+/* ------------------------------------------------------------------------ */
+static void put_node(const or_schema* s, const packos_column* cols, size_t i, int n, or_put* p,
+                     or_put* pool, int depth) {
+    int k = NK(s, n);
+    if (is_container(k)) {
+        int nullable = (k == ORN_MAP) ? 1 : NA(s, n);
+        const packos_column* c = &cols[s->col_of_node[n]];
+        if (nullable && !col_valid(c, i)) { or_put_add_nil(p, leaf_tag(k)); return; } /* AddAnyTuple(nil)/AddMapAny(nil) */
+        or_put* ch = &pool[depth];
+        or_put_reset(ch);
+        or_put_begin(p, leaf_tag(k));
+        int kids[256];
+        int nk = children(s, n, kids);
+        for (int j = 0; j < nk; j++) put_node(s, cols, i, kids[j], ch, pool, depth + 1);
+        or_put_end(p, ch);
+        return;
+    }
+    size_t len; int nil; uint8_t tmp[8];
+    const uint8_t* b = leaf_bytes(s, cols, i, n, &len, &nil, tmp);
+    if (nil) or_put_add_nil(p, leaf_tag(k));
+    else or_put_add(p, leaf_tag(k), b, len);
+}
+
+/* ------------------------------------------------------------------------ */
+/* packable two-pass encode (packable/pack.go:17-67,                          */
+/* packable_mapPackables.go:13-53, packable_nullables.go)                    */
+/* ------------------------------------------------------------------------ */
+static int64_t pk_value_size(const or_schema* s, const packos_column* cols, size_t i, int n) {
+    int k = NK(s, n);
+    if (is_container(k)) {
+        int nullable = (k == ORN_MAP) ? 1 : NA(s, n);
+        if (nullable && !col_valid(&cols[s->col_of_node[n]], i)) return 0;
+        int kids[256];
+        int nk = children(s, n, kids);
+        if (nk == 0) return 0;
+        int64_t sz = 0;
+        for (int j = 0; j < nk; j++) sz += pk_value_size(s, cols, i, kids[j]);
+        return sz + 2 * (int64_t)nk + 2;
+    }
+    size_t len; int nil; uint8_t tmp[8];
+    leaf_bytes(s, cols, i, n, &len, &nil, tmp);
+    return (int64_t)len; /* nullable ValueSize reports full width even for nil */
+}
+
+static int64_t pk_write(const or_schema* s, const packos_column* cols, size_t i, int n, uint8_t* buf,
+                        int64_t pos, int* overflow) {
+    int k = NK(s, n);
+    if (is_container(k)) {
+        int nullable = (k == ORN_MAP) ? 1 : NA(s, n);
+        if (nullable && !col_valid(&cols[s->col_of_node[n]], i)) return pos;
+        int kids[256];
+        int nk = children(s, n, kids);
+        if (nk == 0) return pos;
+        int64_t hsz = 2 * (int64_t)nk + 2, posH = pos;
+        pos += hsz;
+        int64_t delta = pos;
+        for (int j = 0; j < nk; j++) {
+            int64_t off = j == 0 ? hsz : pos - delta;
+            if (ovf(off)) *overflow = 1;
+            wr16(buf + posH, or_encode_header(off, leaf_tag(NK(s, kids[j]))));
+            posH += 2;
+            pos = pk_write(s, cols, i, kids[j], buf, pos, overflow);
+        }
+        if (ovf(pos - delta)) *overflow = 1;
+        wr16(buf + posH, or_encode_header(pos - delta, 0));
+        return pos;
+    }
+    size_t len; int nil; uint8_t tmp[8];
+    const uint8_t* b = leaf_bytes(s, cols, i, n, &len, &nil, tmp);
+    if (nil) return pos; /* WriteNullable*(nil) writes nothing */
+    if (len) memcpy(buf + pos, b, len);
+    return pos + (int64_t)len;
+}
+
+int64_t or_encoded_size_one(const or_schema* s, const packos_column* cols, size_t i, int mode) {
+    if (mode == PACKOS_MODE_PACKABLE) {
+        if (s->n_top == 0) return 0;
+        int64_t sz = 0;
+        for (int t = 0; t < s->n_top; t++) sz += pk_value_size(s, cols, i, s->top_nodes[t]);
+        return sz + 2 * (int64_t)s->n_top + 2;
+    }
+    or_put p, pool[16];
+    or_put_init(&p);
+    for (int d = 0; d < 16; d++) or_put_init(&pool[d]);
+    for (int t = 0; t < s->n_top; t++) put_node(s, cols, i, s->top_nodes[t], &p, pool, 0);
+    int64_t sz = (int64_t)or_put_pack_size(&p);
+    or_put_free(&p);
+    for (int d = 0; d < 16; d++) or_put_free(&pool[d]);
+    return sz;
+}
+
+typedef struct enc_tls { or_put p; or_put pool[16]; } enc_tls;
+
+static int64_t encode_one_tls(const or_schema* s, const packos_column* cols, size_t i, int mode,
+                              uint8_t* out, size_t cap, int* overflow, enc_tls* t) {
+    *overflow = 0;
+    if (mode == PACKOS_MODE_PACKABLE) {
+        /* packable.Pack: buffer of ValueSize() bytes, zero filled (pack.go:59-67) */
+        if (s->n_top == 0) return 0;
+        int64_t size = 0;
+        for (int k = 0; k < s->n_top; k++) size += pk_value_size(s, cols, i, s->top_nodes[k]);
+        size += 2 * (int64_t)s->n_top + 2;
+        if ((size_t)size > cap) return -1;
+        memset(out, 0, (size_t)size);
+        int64_t hsz = 2 * (int64_t)s->n_top + 2, posH = 0, pos = hsz, delta = hsz;
+        for (int k = 0; k < s->n_top; k++) {
+            int n = s->top_nodes[k];
+            int64_t off = k == 0 ? hsz : pos - delta;
+            if (ovf(off)) *overflow = 1;
+            wr16(out + posH, or_encode_header(off, leaf_tag(NK(s, n))));
+            posH += 2;
+            pos = pk_write(s, cols, i, n, out, pos, overflow);
+        }
+        if (ovf(pos - delta)) *overflow = 1;
+        wr16(out + posH, or_encode_header(pos - delta, 0));
+        return size;
+    }
+    or_put_reset(&t->p);
+    for (int k = 0; k < s->n_top; k++) put_node(s, cols, i, s->top_nodes[k], &t->p, t->pool, 0);
+    size_t need = or_put_pack_size(&t->p);
+    if (need > cap) return -1;
+    size_t got = or_put_pack(&t->p, out);
+    *overflow = t->p.overflow;
+    return (int64_t)got;
+}
+
+int64_t or_encode_one(const or_schema* s, const packos_column* cols, size_t i, int mode, uint8_t* out,
+                      size_t cap, int* overflow) {
+    enc_tls t;
+    or_put_init(&t.p);
+    for (int d = 0; d < 16; d++) or_put_init(&t.pool[d]);
+    int64_t r = encode_one_tls(s, cols, i, mode, out, cap, overflow, &t);
+    or_put_free(&t.p);
+    for (int d = 0; d < 16; d++) or_put_free(&t.pool[d]);
+    return r;
+}
+
+typedef struct enc_job {
+    const or_schema* s; const packos_column* cols; int mode;
+    uint8_t* out; uint64_t* offs; uint32_t* status; size_t lo, hi;
+} enc_job;
+
+static void* enc_worker(void* arg) {
+    enc_job* j = (enc_job*)arg;
+    enc_tls t;
+    or_put_init(&t.p);
+    for (int d = 0; d < 16; d++) or_put_init(&t.pool[d]);
+    for (size_t i = j->lo; i < j->hi; i++) {
+        int o = 0;
+        size_t cap = (size_t)(j->offs[i + 1] - j->offs[i]);
+        encode_one_tls(j->s, j->cols, i, j->mode, j->out + j->offs[i], cap, &o, &t);
+        if (j->status) j->status[i] = o ? PACKOS_STATUS_OVERFLOW13 : 0u;
+    }
+    or_put_free(&t.p);
+    for (int d = 0; d < 16; d++) or_put_free(&t.pool[d]);
+    return NULL;
+}
+
+typedef struct size_job { const or_schema* s; const packos_column* cols; int mode; uint64_t* offs; size_t lo, hi; } size_job;
+static void* size_worker(void* arg) {
+    size_job* j = (size_job*)arg;
+    for (size_t i = j->lo; i < j->hi; i++) j->offs[i + 1] = (uint64_t)or_encoded_size_one(j->s, j->cols, i, j->mode);
+    return NULL;
+}
+
+int64_t or_encode_batch(const or_schema* s, const packos_column* cols, size_t n, int mode, uint8_t* out,
+                        size_t cap, uint64_t* out_offsets, uint32_t* status, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    size_job sj[256];
+    size_t per = (n + (size_t)nthreads - 1) / (size_t)nthreads;
+    out_offsets[0] = 0;
+    for (int t = 0; t < nthreads; t++) {
+        size_t lo = (size_t)t * per, hi = lo + per > n ? n : lo + per;
+        if (lo > hi) lo = hi;
+        sj[t] = (size_job){s, cols, mode, out_offsets, lo, hi};
+        pthread_create(&th[t], NULL, size_worker, &sj[t]);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    for (size_t i = 0; i < n; i++) out_offsets[i + 1] += out_offsets[i];
+    if (out_offsets[n] > cap) return -1;
+    enc_job ej[256];
+    for (int t = 0; t < nthreads; t++) {
+        size_t lo = (size_t)t * per, hi = lo + per > n ? n : lo + per;
+        if (lo > hi) lo = hi;
+        ej[t] = (enc_job){s, cols, mode, out, out_offsets, status, lo, hi};
+        pthread_create(&th[t], NULL, enc_worker, &ej[t]);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    return (int64_t)out_offsets[n];
+}
+
+/* ------------------------------------------------------------------------ */
+/* SeqGetAccess (access/seqget.go:22-154)                                    */
+/* ------------------------------------------------------------------------ */
+int or_seq_init(or_seq* s, const uint8_t* buf, int64_t len) {
+    if (len < 4) return 1;                     /* "insufficient header" */
+    uint16_t h0 = rd16(buf);
+    int64_t base = h0 >> 3;
+    if (len < base) return 1;
+    uint16_t h1 = rd16(buf + 2);
+    s->buf = buf; s->len = len;
+    s->base = base; s->count = base / 2; s->pos = 0;
+    s->cur_off = base; s->cur_type = h0 & 7;
+    s->next_off = (h1 >> 3) + base; s->next_type = h1 & 7;
+    return 0;
+}
+int or_seq_peek(const or_seq* s, int* typ, int64_t* width) {
+    if (s->pos >= s->count) return 1;
+    *typ = s->cur_type;
+    if (s->next_off > s->len) { *width = -1; return 1; }
+    *width = s->next_off - s->cur_off;
+    return 0;
+}
+int or_seq_advance(or_seq* s) {
+    if (s->pos + 2 > s->count) return 1;
+    s->pos++;
+    s->cur_off = s->next_off;
+    s->cur_type = s->next_type;
+    if (s->cur_type != 0) {
+        uint16_t h = rd16(s->buf + (s->pos + 1) * 2);
+        s->next_off = (h >> 3) + s->base;
+        s->next_type = h & 7;
+    }
+    return 0;
+}
+int or_seq_next(or_seq* s, int64_t* start, int64_t* width, int* typ) {
+    int64_t w;
+    if (or_seq_peek(s, typ, &w)) return 1;
+    if (w < 0 || s->cur_off + w > s->len) return 1;
+    *start = s->cur_off; *width = w;
+    return or_seq_advance(s);
+}
+int or_seq_peek_nested(const or_seq* s, or_seq* nested) {
+    if (s->cur_type != 7 && s->cur_type != 4) return 1;
+    int64_t w = s->next_off - s->cur_off;
+    if (w <= 0 || s->next_off > s->len) return 1;
+    return or_seq_init(nested, s->buf + s->cur_off, w);
+}
+
+/* ------------------------------------------------------------------------ */
+/* schema decode (schema/schema.go:893-910, 997-1052, 594-829, 270-326,      */
+/* 383-414, 1591-1633, 1062-1130 Match)                                       */
+/* ------------------------------------------------------------------------ */
+#define DEC_PANIC 0x100
+
+typedef struct dec_ctx {
+    const or_schema* s; packos_column* cols; size_t i; uint64_t blob_base;
+} dec_ctx;
+
+/* precheck (schema.go:997-1013): 0 ok, else ErrConstraintViolated */
+static int precheck(const or_seq* q, int tag, int64_t hint, int nullable, int64_t* w) {
+    int typ; int64_t width;
+    if (or_seq_peek(q, &typ, &width)) return 3;
+    if (typ != tag) return 3;
+    if (!nullable && hint != 0 && width != hint) return 3;
+    *w = width;
+    return 0;
+}
+
+/* validatePrimitiveAndGetPayload (schema.go:1031-1052): returns code,
+ * *ps = payload start (-1 = nil payload), *w = width                        */
+static int prim(or_seq* q, int tag, int64_t hint, int nullable, int64_t* ps, int64_t* w) {
+    int e = precheck(q, tag, hint, nullable, w);
+    if (e) return e;
+    *ps = -1;
+    if (*w > 0) {
+        if (q->cur_off + *w > q->len) return 1;
+        *ps = q->cur_off;
+    }
+    if (or_seq_advance(q)) return 2;
+    return 0;
+}
+
+static int dec_node(dec_ctx* c, int n, or_seq* q, uint64_t sub_base) {
+    const or_schema* s = c->s;
+    int k = NK(s, n);
+    packos_column* col = s->col_of_node[n] >= 0 ? &c->cols[s->col_of_node[n]] : NULL;
+    int64_t ps, w;
+    switch (k) {
+        case ORN_INT: case ORN_UINT: case ORN_FLOAT: case ORN_BOOL: {
+            int W = NA(s, n), nul = NB(s, n);
+            int e = prim(q, leaf_tag(k), W, nul, &ps, &w);
+            if (e) return e;
+            if (ps < 0) { if (col->valid) col->valid[c->i] = 0; return 0; }
+            if (w < W) return DEC_PANIC; /* binary.LittleEndian.UintXX on a short slice panics */
+            uint8_t* dst = (uint8_t*)col->data + c->i * (size_t)W;
+            if (k == ORN_BOOL) dst[0] = q->buf[ps] != 0;
+            else memcpy(dst, q->buf + ps, (size_t)W);
+            if (col->valid) col->valid[c->i] = 1;
+            return 0;
+        }
+        case ORN_STRING: case ORN_BYTES: {
+            int W = NA(s, n);
+            int e = prim(q, 6, W, W <= 0, &ps, &w);
+            if (e) return e;
+            if (W > 0) {
+                memcpy((uint8_t*)col->data + c->i * (size_t)W, q->buf + ps, (size_t)W);
+            } else {
+                /* aliasing view like GetStringUnsafe: absolute payload start, 0 for nil */
+                col->start[c->i] = ps < 0 ? 0u : sub_base + (uint64_t)ps;
+                col->length[c->i] = ps < 0 ? 0u : (uint32_t)w;
+            }
+            return 0;
+        }
+        case ORN_MATCH: {
+            /* SString.Match(expected): CheckFunc DecodeFunc (schema.go:1092-1108) */
+            int e = prim(q, 6, 0, 1, &ps, &w);
+            if (e) return e;
+            size_t ll; const uint8_t* lp = lit_ptr(s, NA(s, n), &ll);
+            size_t have = ps < 0 ? 0 : (size_t)w;
+            if (have != ll || (ll && memcmp(q->buf + ps, lp, ll) != 0)) return PACKOS_ERR_STRING_MATCH;
+            return 0;
+        }
+        case ORN_TUPLE: case ORN_MAP: {
+            int nul = (k == ORN_MAP) ? 1 : NA(s, n);
+            int e = precheck(q, leaf_tag(k), -1, nul, &w);
+            if (e) return e;
+            int kids[256];
+            int nk = children(s, n, kids);
+            if (k == ORN_MAP && (nk % 2) != 0) return 3; /* SizeExact (schema.go:395-403) */
+            if (w != 0) {
+                or_seq sub;
+                if (or_seq_peek_nested(q, &sub)) return 1;
+                if (k == ORN_TUPLE && nk > 0 && (sub.count - 1) != nk && !NC(s, n)) return 3;
+                uint64_t nb = sub_base + (uint64_t)q->cur_off;
+                for (int j = 0; j < nk; j++) {
+                    int ce = dec_node(c, kids[j], &sub, nb);
+                    if (ce == DEC_PANIC) return DEC_PANIC;
+                    if (ce) return 1; /* wrapped as ErrInvalidFormat */
+                }
+            }
+            if (col && col->valid) col->valid[c->i] = w != 0;
+            if (or_seq_advance(q)) return 2;
+            return 0;
+        }
+    }
+    return 1;
+}
+
+static uint32_t decode_one(const or_schema* s, const uint8_t* blob, int64_t len, uint64_t base,
+                           packos_column* cols, size_t i) {
+    or_seq q;
+    if (or_seq_init(&q, blob, len)) return (uint32_t)PACKOS_ERR_INVALID_FORMAT; /* pos -1 */
+    dec_ctx c = {s, cols, i, base};
+    for (int t = 0; t < s->n_top; t++) {
+        int e = dec_node(&c, s->top_nodes[t], &q, base);
+        if (e == DEC_PANIC) return PACKOS_STATUS_PANIC | ((uint32_t)(t + 1) << 8);
+        if (e) return (uint32_t)e | ((uint32_t)(t + 1) << 8);
+    }
+    return 0;
+}
+
+typedef struct dec_job {
+    const or_schema* s; const uint8_t* arena; const uint64_t* offs; uint64_t stride;
+    packos_column* cols; uint32_t* status; size_t lo, hi;
+} dec_job;
+static void* dec_worker(void* arg) {
+    dec_job* j = (dec_job*)arg;
+    for (size_t i = j->lo; i < j->hi; i++) {
+        uint64_t a = j->offs ? j->offs[i] : i * j->stride;
+        uint64_t b = j->offs ? j->offs[i + 1] : (i + 1) * j->stride;
+        j->status[i] = decode_one(j->s, j->arena + a, (int64_t)(b - a), a, j->cols, i);
+    }
+    return NULL;
+}
+int or_decode_batch(const or_schema* s, const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
+                    size_t n, packos_column* cols, uint32_t* status, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    dec_job dj[256];
+    size_t per = (n + (size_t)nthreads - 1) / (size_t)nthreads;
+    for (int t = 0; t < nthreads; t++) {
+        size_t lo = (size_t)t * per, hi = lo + per > n ? n : lo + per;
+        if (lo > hi) lo = hi;
+        dj[t] = (dec_job){s, arena, offsets, stride, cols, status, lo, hi};
+        pthread_create(&th[t], NULL, dec_worker, &dj[t]);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* GetAccess (access/get.go:19-58, 60-375, 492-501)                          */
+/* ------------------------------------------------------------------------ */
+int or_get_init(or_get* g, const uint8_t* buf, int64_t len) {
+    if (len < 2) return 0;
+    int64_t base = rd16(buf) >> 3;
+    if (len < base) return 0;
+    g->buf = buf; g->len = len; g->base = base; g->arg_count = base / 2 - 1;
+    return 1;
+}
+void or_get_range(const or_get* g, int64_t pos, int* tp, int64_t* start, int64_t* end) {
+    if (pos >= g->arg_count) { *tp = 0; *start = -2; *end = -1; return; }
+    uint16_t h1 = rd16(g->buf + pos * 2), h2 = rd16(g->buf + (pos + 1) * 2);
+    *start = h1 >> 3; *tp = h1 & 7;
+    *end = (h2 >> 3) + g->base;
+    if (pos > 0) *start += g->base;
+    if (*end > g->len) *end = -1;
+}
+int or_get_fixed(const or_get* g, int64_t pos, int tag, int width, int64_t* start) {
+    int tp; int64_t st, en;
+    or_get_range(g, pos, &tp, &st, &en);
+    if (tp != tag || en - st != width) return 1;
+    *start = st;
+    return 0;
+}
+int or_get_nullable(const or_get* g, int64_t pos, int tag, int width, int64_t* start) {
+    int tp; int64_t st, en;
+    or_get_range(g, pos, &tp, &st, &en);
+    if (en - st == 0) return 2;
+    if (tp != tag || en - st != width) return 1;
+    *start = st;
+    return 0;
+}
+int or_get_span(const or_get* g, int64_t pos, int64_t* start, int64_t* end) {
+    int tp; int64_t st, en;
+    or_get_range(g, pos, &tp, &st, &en);
+    if (tp != 6 || en < st) return 1;
+    *start = st; *end = en;
+    return 0;
+}
+int or_get_nested(const or_get* g, int64_t pos, or_get* nested, int* tp) {
+    int64_t st, en;
+    or_get_range(g, pos, tp, &st, &en);
+    if (en < st || (*tp != 7 && *tp != 4)) return 1;
+    if (en == st) return 2;
+    if (!or_get_init(nested, g->buf + st, en - st)) return 3; /* nil accessor: later use panics */
+    return 0;
+}
+
+int or_get_field_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride, size_t n,
+                       const int32_t* path, int depth, int want_tag, int want_width,
+                       uint64_t* out_start, uint32_t* out_len, uint8_t* out_tag, uint8_t* status) {
+    for (size_t i = 0; i < n; i++) {
+        uint64_t a = offsets ? offsets[i] : i * stride;
+        uint64_t b = offsets ? offsets[i + 1] : (i + 1) * stride;
+        or_get g;
+        out_start[i] = 0; out_len[i] = 0; out_tag[i] = 0;
+        if (!or_get_init(&g, arena + a, (int64_t)(b - a))) { status[i] = 3; continue; }
+        uint64_t base = a;
+        int st = 0;
+        for (int d = 0; d < depth - 1 && !st; d++) {
+            or_get nx; int tp;
+            int r = or_get_nested(&g, path[d], &nx, &tp);
+            if (r) { st = r; break; }
+            base += (uint64_t)(nx.buf - g.buf);
+            g = nx;
+        }
+        if (st) { status[i] = (uint8_t)st; continue; }
+        int tp; int64_t s0, e0;
+        or_get_range(&g, path[depth - 1], &tp, &s0, &e0);
+        out_tag[i] = (uint8_t)tp;
+        if (want_width >= 0) {
+            if (tp != want_tag || e0 - s0 != want_width) { status[i] = 1; continue; }
+        } else {
+            if (tp != want_tag || e0 < s0) { status[i] = 1; continue; }
+        }
+        out_start[i] = base + (uint64_t)s0;
+        out_len[i] = (uint32_t)(e0 - s0);
+        status[i] = 0;
+    }
+    return 0;
+}
+
+uint64_t or_splitmix64(uint64_t* state) {
+    uint64_t z = (*state += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}

@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""Build tests/golden/vectors.json from the reference's own tests.
+
+Byte vectors are EXTRACTED from the reference test sources under
+/root/reference (the `expected := []byte{...}` / `buf := []byte{...}` blocks
+of access/put_test.go, packable/pack_test.go, access/get_test.go,
+access/seqget_test.go and README.md): the parser below reads the hex and char
+literals of the block that starts at the cited line.  What each test FEEDS the
+API (the Add*/Pack* call sequence or the schema + value) is transcribed by
+hand into the CASES table as a schema (SchemaJSON vocabulary) plus one row
+value, with the same file:line citation.
+
+Cross-API equalities the reference asserts without spelling out bytes
+(e.g. schema.EncodeValue == packable.Pack) are recorded as "equal" groups.
+
+The reference is Go and no Go toolchain exists in this image, so nothing here
+runs the reference; the JSON is data only.  Run: python tests/golden/make_golden.py
+"""
+import json
+import os
+import re
+import sys
+
+REF = "/root/reference"
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "vectors.json")
+
+
+def extract_bytes(relpath, line):
+    """Hex/char literals of the []byte{...} block starting at `line` (1-based)."""
+    with open(os.path.join(REF, relpath), encoding="utf-8") as f:
+        lines = f.read().split("\n")
+    i = line - 1
+    if "[]byte{" not in lines[i]:
+        raise ValueError(f"{relpath}:{line} is not a []byte{{ block: {lines[i]!r}")
+    out = []
+    depth = 0
+    first = True
+    while True:
+        ln = lines[i]
+        code = ln.split("//", 1)[0]
+        if first:
+            code = code.split("[]byte{", 1)[1]
+            depth = 1
+            first = False
+        for tok in re.finditer(r"0x[0-9A-Fa-f]{1,2}|'(\\.|[^'])'|[{}]", code):
+            t = tok.group(0)
+            if t == "{":
+                depth += 1
+            elif t == "}":
+                depth -= 1
+                if depth == 0:
+                    return bytes(out)
+            elif t.startswith("0x"):
+                out.append(int(t, 16))
+            else:
+                ch = tok.group(1)
+                out.append(ord(ch.encode().decode("unicode_escape")))
+        i += 1
+
+
+def S(x):
+    return {"s": x}
+
+
+def B(x):
+    return {"b": x.encode().hex() if isinstance(x, str) else x.hex()}
+
+
+def F32(x):
+    return {"f32": x}
+
+
+# SchemaJSON snippets
+I16 = {"type": "int16"}
+I32 = {"type": "int32"}
+I64 = {"type": "int64"}
+F32T = {"type": "float32"}
+BOOL = {"type": "bool"}
+STR = {"type": "string"}
+BYT = {"type": "bytes"}
+
+
+def EX(k):
+    return {"type": "string", "exact": k}
+
+
+def MAP(*kv, sorted_=False):
+    d = {"type": "map", "schema": list(kv)}
+    if sorted_:
+        d["sorted"] = True
+    return d
+
+
+def TUP(*kids, names=None):
+    d = {"type": "tuple", "schema": list(kids)}
+    if names is not None:
+        d["fieldNames"] = names
+    return d
+
+
+META_SORTED = MAP(EX("user"), BYT, EX("role"), BYT, sorted_=True)
+META_ORDERED = MAP(EX("role"), BYT, EX("user"), BYT)
+ROW_META = {"user": B("alice"), "role": B("admin")}
+
+ENCODE = [
+    # id, source, mode, schema, row, bytes-source
+    ("put_flat17", "access/put_test.go:12-41", "putaccess", [I16, BOOL, STR, BYT],
+     [42, True, S("go"), B(b"\xaa\xbb")], ("access/put_test.go", 22)),
+    ("put_map_sorted32", "access/put_test.go:44-75", "putaccess",
+     [MAP(EX("user"), BYT, EX("role"), BYT, sorted_=True)], [ROW_META],
+     ("access/put_test.go", 53)),
+    ("put_int_nested_sorted60", "access/put_test.go:78-135", "putaccess",
+     [I16, MAP(EX("meta"), META_SORTED, EX("name"), STR, sorted_=True)],
+     [12345, {"meta": ROW_META, "name": S("gopher")}], ("access/put_test.go", 91)),
+    ("put_nullables23", "access/put_test.go:138-177", "putaccess",
+     [{"type": "int32", "nullable": True}, {"type": "int32", "nullable": True},
+      {"type": "float32", "nullable": True}, {"type": "float32", "nullable": True},
+      {"type": "bool", "nullable": True}, {"type": "bool", "nullable": True}],
+     [None, 123456, None, F32(3.14159), None, True], ("access/put_test.go", 154)),
+    ("put_ordered60", "access/put_test.go:180-245", "putaccess",
+     [I16, MAP(EX("meta"), META_ORDERED, EX("name"), STR)],
+     [12345, {"meta": ROW_META, "name": S("gopher")}], ("access/put_test.go", 202)),
+    ("pack_flat17", "packable/pack_test.go:12-40", "packable", [I16, BOOL, STR, BYT],
+     [42, True, S("go"), B(b"\xaa\xbb")], ("packable/pack_test.go", 17)),
+    ("pack_sorted60", "packable/pack_test.go:42-97", "packable",
+     [I16, MAP(EX("meta"), META_SORTED, EX("name"), STR, sorted_=True)],
+     [12345, {"meta": ROW_META, "name": S("gopher")}], ("packable/pack_test.go", 54)),
+    ("pack_two_tuples34", "packable/pack_test.go:120-171", "packable",
+     [TUP(I32, BOOL, STR), TUP(I16, BOOL, STR)],
+     [[2025, False, S("az")], [7, True, S("go")]], ("packable/pack_test.go", 134)),
+    ("pack_ordered60", "packable/pack_test.go:173-232", "packable",
+     [I16, MAP(EX("meta"), META_ORDERED, EX("name"), STR)],
+     [12345, {"meta": ROW_META, "name": S("gopher")}], ("packable/pack_test.go", 191)),
+    ("readme_flat17", "README.md:43-65", "putaccess", [I16, BOOL, STR, BYT],
+     [42, True, S("go"), B(b"\xaa\xbb")], ("README.md", 52)),
+    ("readme_sorted60", "README.md:69-115", "packable",
+     [I16, MAP(EX("meta"), META_SORTED, EX("name"), STR, sorted_=True)],
+     [12345, {"meta": ROW_META, "name": S("gopher")}], ("README.md", 80)),
+    ("readme_two_tuples34", "README.md:119-156", "packable",
+     [TUP(I32, BOOL, STR), TUP(I16, BOOL, STR)],
+     [[2025, False, S("az")], [7, True, S("go")]], ("README.md", 132)),
+    # schema.EncodeValue of the two tuples must give pack_test's bytes
+    ("schema_two_tuples34", "schema/schema_test.go:781-818 (expected = pack.Pack(...) = packable/pack_test.go:134)",
+     "putaccess",
+     [TUP(I32, BOOL, {"type": "string", "width": 2}), TUP(I16, BOOL, {"type": "string", "width": 2})],
+     [[2025, False, S("az")], [7, True, S("go")]], ("packable/pack_test.go", 134)),
+    ("schema_named_tuples34", "schema/schema_test.go:1248-1303 (expected = packable/pack_test.go:134)",
+     "putaccess",
+     {"type": "chain", "fieldNames": ["firstTuple", "secondTuple"], "schema": [
+         TUP(I32, BOOL, {"type": "string", "width": 2}, names=["year", "flag", "code"]),
+         TUP(I16, BOOL, {"type": "string", "width": 2}, names=["num", "flag", "lang"])]},
+     {"firstTuple": {"year": 2025, "flag": False, "code": S("az")},
+      "secondTuple": {"num": 7, "flag": True, "lang": S("go")}}, ("packable/pack_test.go", 134)),
+]
+
+# groups whose encodings the reference asserts equal (no literal bytes)
+EQUAL = [
+    ("putaccess_addpackable_eq_pack", "packable/pack_test.go:99-118", [
+        ("putaccess", [I16, MAP(EX("meta"), META_SORTED, EX("name"), STR, sorted_=True), F32T]),
+        ("packable", [I16, MAP(EX("meta"), META_SORTED, EX("name"), STR, sorted_=True), F32T])],
+     [12345, {"meta": ROW_META, "name": S("gopher")}, F32(4.45)]),
+    ("putaccess_addpackable_ordered_eq_pack", "packable/pack_test.go:234-256", [
+        ("putaccess", [I16, MAP(EX("meta"), META_ORDERED, EX("name"), STR), F32T]),
+        ("packable", [I16, MAP(EX("meta"), META_ORDERED, EX("name"), STR), F32T])],
+     [12345, {"meta": ROW_META, "name": S("gopher")}, F32(4.45)]),
+    ("schema_empty_tuples1", "schema/schema_test.go:820-839", [
+        ("putaccess", [TUP(), TUP()]),
+        ("packable", [TUP(), TUP()])],
+     [None, None]),
+    ("schema_empty_tuples2", "schema/schema_test.go:840-869", [
+        ("putaccess", [I16, TUP(STR, STR, STR), TUP(), TUP(STR, names=["ok"]), TUP(names=[]), I16]),
+        ("packable", [I16, TUP(), TUP(), TUP(), TUP(), I16])],
+     [5, None, None, None, None, 5]),
+    ("schema_empty_maps", "schema/schema_test.go:870-911 (SMap subset)", [
+        ("putaccess", [I16, MAP(STR, STR), MAP(STR, STR), MAP(STR, STR), I16]),
+        ("packable", [I16, MAP(), MAP(), MAP(), I16])],
+     [5, None, None, None, 5]),
+    ("schema_packed_structure", "schema/schema_test.go:1116-1173", [
+        ("putaccess", [I16, F32T, I64, BOOL,
+                       MAP(EX("meta"), MAP(EX("role"), {"type": "bytes", "width": 5},
+                                           EX("user"), {"type": "bytes", "width": 5}),
+                           EX("name"), {"type": "string", "width": 6})]),
+        ("packable", [I16, F32T, I64, BOOL,
+                      MAP(EX("meta"), META_SORTED, EX("name"), STR, sorted_=True)])],
+     [12345, F32(3.14), 9876543210, True, {"meta": ROW_META, "name": S("gopher")}]),
+]
+
+# random-access known answers: (pos path, want_tag, want_width, expected payload)
+GET = [
+    ("get_flat", "access/get_test.go:11-44", ("access/get_test.go", 12), [
+        ([0], 1, 2, "2a00"), ([1], 5, 1, "01"), ([2], 6, -1, b"go".hex()), ([3], 6, -1, "aabb")]),
+    ("get_map2", "access/get_test.go:46-63", ("access/get_test.go", 47), [
+        ([0, 0], 6, -1, b"role".hex()), ([0, 1], 6, -1, b"admin".hex()),
+        ([0, 2], 6, -1, b"user".hex()), ([0, 3], 6, -1, b"alice".hex())]),
+    ("get_map_ordered", "access/get_test.go:65-96", ("access/get_test.go", 66), [
+        ([0, 0], 6, -1, b"role".hex()), ([0, 3], 6, -1, b"alice".hex())]),
+    ("get_int_then_map", "access/get_test.go:98-126", ("access/get_test.go", 99), [
+        ([0], 1, 2, "3930"), ([1, 0], 6, -1, b"meta".hex()), ([1, 1, 1], 6, -1, b"admin".hex()),
+        ([1, 1, 3], 6, -1, b"alice".hex()), ([1, 2], 6, -1, b"name".hex()),
+        ([1, 3], 6, -1, b"gopher".hex())]),
+]
+
+SEQ = [
+    ("seq_nested_map", "access/seqget_test.go:11-101", ("access/seqget_test.go", 12)),
+    ("seq_flat_end", "access/seqget_test.go:103-151", ("access/seqget_test.go", 104)),
+]
+
+# schema.DecodeBuffer known answers over bytes produced by the encoders above
+DECODE = [
+    ("decode_packed_structure", "schema/schema_test.go:244-316", "schema_packed_structure",
+     [I16, F32T, I64, BOOL, MAP(EX("meta"), MAP(EX("role"), {"type": "bytes", "width": 5},
+                                               EX("user"), {"type": "bytes", "width": 5}),
+                               EX("name"), {"type": "string", "width": 6})],
+     [12345, F32(3.14), 9876543210, True, {"meta": {"role": B("admin"), "user": B("alice")},
+                                          "name": S("gopher")}], 0),
+    ("decode_two_tuples", "schema/schema_test.go:363-404", "pack_two_tuples34",
+     [TUP(I32, BOOL, {"type": "string", "width": 2}), TUP(I16, BOOL, {"type": "string", "width": 2})],
+     [[2025, False, S("az")], [7, True, S("go")]], 0),
+    ("decode_empty_tuples2", "schema/schema_test.go:840-869", "schema_empty_tuples2",
+     [I16, TUP(STR, STR, STR), TUP(), TUP(STR, names=["ok"]), TUP(names=[]), I16],
+     [5, None, None, None, None, 5], 0),
+    # wrong width for "admin": SBytes(6) -> error (ValidateBuffer fails; DecodeBuffer
+    # reports the SMap at top-level position 4 wrapping ErrInvalidFormat)
+    ("decode_failure_width", "schema/schema_test.go:52-89", "schema_packed_structure",
+     [I16, F32T, I64, BOOL, MAP(EX("meta"), MAP(EX("role"), {"type": "bytes", "width": 6},
+                                               EX("user"), {"type": "bytes", "width": 5}),
+                               EX("name"), {"type": "string", "width": 6})],
+     None, (1 | (5 << 8))),
+]
+
+
+def main():
+    if not os.path.isdir(REF):
+        sys.exit("reference not present; vectors.json is already committed")
+    out = {"note": __doc__.strip().split("\n")[0], "encode": [], "equal": [], "get": [], "seq": [],
+           "decode": []}
+    for cid, src, mode, schema, row, (bf, bl) in ENCODE:
+        out["encode"].append({"id": cid, "source": src, "mode": mode, "schema": schema, "row": row,
+                              "bytes_from": f"{bf}:{bl}", "hex": extract_bytes(bf, bl).hex()})
+    for cid, src, variants, row in EQUAL:
+        out["equal"].append({"id": cid, "source": src, "row": row,
+                             "variants": [{"mode": m, "schema": s} for m, s in variants]})
+    for cid, src, (bf, bl), queries in GET:
+        out["get"].append({"id": cid, "source": src, "bytes_from": f"{bf}:{bl}",
+                           "hex": extract_bytes(bf, bl).hex(),
+                           "queries": [{"path": p, "tag": t, "width": w, "expect": e}
+                                       for p, t, w, e in queries]})
+    for cid, src, (bf, bl) in SEQ:
+        out["seq"].append({"id": cid, "source": src, "bytes_from": f"{bf}:{bl}",
+                           "hex": extract_bytes(bf, bl).hex()})
+    for cid, src, from_case, schema, row, status in DECODE:
+        out["decode"].append({"id": cid, "source": src, "input_from": from_case, "schema": schema,
+                              "expect_row": row, "expect_status": status})
+    with open(OUT, "w") as f:
+        json.dump(out, f, indent=1)
+    print(f"wrote {OUT}: {len(out['encode'])} encode, {len(out['equal'])} equal, "
+          f"{len(out['get'])} get, {len(out['seq'])} seq, {len(out['decode'])} decode")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,132 @@
+"""Pin the CPU oracle to the reference's own golden vectors (CPU only).
+
+Every byte vector comes from the reference test sources via
+tests/golden/make_golden.py; a failure here means the oracle is not a faithful
+restatement and no GPU parity claim can rest on it.
+"""
+import numpy as np
+import pytest
+
+import oracle_bridge as ob
+from golden_util import MODES, chain_of, load, unwrap
+from packos_amd.columns import HostColumns, column_specs
+
+G = load()
+
+
+def _encode_one(schema_json, row, mode):
+    chain = chain_of(schema_json)
+    hc = HostColumns.from_rows(chain, [unwrap(row)])
+    arena, offs, st = ob.encode(chain, hc, mode)
+    return bytes(arena[int(offs[0]):int(offs[1])]), int(st[0])
+
+
+@pytest.mark.parametrize("case", G["encode"], ids=[c["id"] for c in G["encode"]])
+def test_encode_golden(case):
+    got, st = _encode_one(case["schema"], case["row"], MODES[case["mode"]])
+    assert got.hex() == case["hex"], f"{case['id']} ({case['source']})"
+    assert st == 0
+
+
+@pytest.mark.parametrize("case", G["equal"], ids=[c["id"] for c in G["equal"]])
+def test_cross_api_equal(case):
+    outs = [_encode_one(v["schema"], case["row"], MODES[v["mode"]])[0] for v in case["variants"]]
+    for o in outs[1:]:
+        assert o == outs[0], f"{case['id']} ({case['source']})"
+
+
+def test_empty_tuple_bytes():
+    # schema_test.go:820: EncodeValue(nil, nil tuples) == Pack(PackTuple(), PackTuple())
+    case = next(c for c in G["equal"] if c["id"] == "schema_empty_tuples1")
+    got, _ = _encode_one(case["variants"][0]["schema"], case["row"], 0)
+    assert got == bytes.fromhex("340004000000")
+
+
+@pytest.mark.parametrize("case", G["get"], ids=[c["id"] for c in G["get"]])
+def test_getaccess_golden(case):
+    buf = np.frombuffer(bytes.fromhex(case["hex"]), np.uint8)
+    offs = np.asarray([0, buf.size], np.uint64)
+    for q in case["queries"]:
+        s0, ln, tg, st = ob.get_field_batch(buf, offs, 1, q["path"], q["tag"], q["width"])
+        assert st[0] == 0, q
+        assert bytes(buf[int(s0[0]):int(s0[0]) + int(ln[0])]).hex() == q["expect"], q
+
+
+def test_getaccess_wrong_type_and_width():
+    case = next(c for c in G["get"] if c["id"] == "get_flat")
+    buf = np.frombuffer(bytes.fromhex(case["hex"]), np.uint8)
+    offs = np.asarray([0, buf.size], np.uint64)
+    # GetInt32(0) on an int16 field -> decode error (tag ok, width 2 != 4)
+    assert ob.get_field_batch(buf, offs, 1, [0], 1, 4)[3][0] == 1
+    # GetBool(0) -> wrong tag
+    assert ob.get_field_batch(buf, offs, 1, [0], 5, 1)[3][0] == 1
+    # position past argCount -> rangeAt returns TypeEnd
+    assert ob.get_field_batch(buf, offs, 1, [4], 1, 2)[3][0] == 1
+    # nested access on a scalar -> "it's not nested type"
+    assert ob.get_field_batch(buf, offs, 1, [0, 0], 6, -1)[3][0] == 1
+
+
+def test_seqget_nested_map_golden():
+    # access/seqget_test.go:11-101
+    case = next(c for c in G["seq"] if c["id"] == "seq_nested_map")
+    s = ob.Seq(bytes.fromhex(case["hex"]))
+    assert s.err == 0
+    p, t, e = s.next()
+    assert (p, t, e) == (bytes([0x39, 0x30]), 1, False)
+    t, w, e = s.peek()
+    assert (t, w, e) == (7, 52, False)
+    nested = s.nested()
+    assert nested is not None
+    p, t, e = nested.next()
+    assert (p, t) == (b"meta", 6)
+    meta = nested.nested()
+    assert meta.next()[:2] == (b"role", 6)
+    assert meta.next()[:2] == (b"admin", 6)
+    assert nested.advance()
+    assert nested.next()[:2] == (b"name", 6)
+    assert nested.next()[:2] == (b"gopher", 6)
+
+
+def test_seqget_flat_end_golden():
+    # access/seqget_test.go:103-151: four fields then End -> error
+    case = next(c for c in G["seq"] if c["id"] == "seq_flat_end")
+    s = ob.Seq(bytes.fromhex(case["hex"]))
+    assert s.next()[:2] == (bytes([0x2A, 0x00]), 1)
+    assert s.next()[:2] == (bytes([0x01]), 5)
+    assert s.next()[:2] == (b"go", 6)
+    assert s.next()[:2] == (bytes([0xAA, 0xBB]), 6)
+    p, t, err = s.next()
+    assert t == 0 and err
+
+
+def _golden_bytes(case_id):
+    for c in G["encode"]:
+        if c["id"] == case_id:
+            return bytes.fromhex(c["hex"])
+    eq = next(c for c in G["equal"] if c["id"] == case_id)
+    v = eq["variants"][0]
+    return _encode_one(v["schema"], eq["row"], MODES[v["mode"]])[0]
+
+
+@pytest.mark.parametrize("case", G["decode"], ids=[c["id"] for c in G["decode"]])
+def test_decode_golden(case):
+    blob = _golden_bytes(case["input_from"])
+    chain = chain_of(case["schema"])
+    arena = np.frombuffer(blob, np.uint8)
+    out, st = ob.decode(chain, arena, np.asarray([0, len(blob)], np.uint64), 1)
+    assert int(st[0]) == case["expect_status"], hex(int(st[0]))
+    if case["expect_row"] is None:
+        return
+    # re-encoding the decoded columns must reproduce the expected row's encoding
+    exp = HostColumns.from_rows(chain, [unwrap(case["expect_row"])])
+    for c, sp in enumerate(column_specs(chain)):
+        if sp.fixed:
+            valid = exp.valid[c] is None or exp.valid[c][0]
+            if valid:
+                assert bytes(out.data[c][:sp.width]) == bytes(exp.data[c][:sp.width]), sp.path
+        if sp.has_valid:
+            assert int(out.valid[c][0]) == int(exp.valid[c][0]), (c, sp.kind)
+        if sp.var:
+            s0, ln = int(out.start[c][0]), int(out.length[c][0])
+            o = exp.offsets[c]
+            assert blob[s0:s0 + ln] == bytes(exp.data[c][o[0]:o[1]])
