@@ -1,0 +1,247 @@
+#!/usr/bin/env python3
+"""Device-resident bulk PackOS encode throughput (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config M|C2|C3|C4|C5] [--e2e]
+
+One step = one encode launch over the whole per-GPU batch with inputs already
+resident in HBM (metric config M: 1M x 256 B fixed-schema tuples per GPU).
+N>1: launched by torch.distributed.run, one rank per GPU; blobs are
+independent, so every rank encodes its own shard (seed + rank) with no data-
+path collective (weak scaling).  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md), GB/s
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", default="M")
+    p.add_argument("--n", type=int, default=0, help="blobs per GPU (default: the config's)")
+    p.add_argument("--e2e", action="store_true", help="also time pinned H2D + encode + D2H")
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    return p.parse_args()
+
+
+def cpu_baseline(cfg, hc, seconds):
+    """CPU oracle (a C restatement of the reference encoder, 'port') timed on
+    this host's cores over repeated passes of the rank-0 sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bridge as ob  # checker / baseline only
+    threads = max(1, min(16, os.cpu_count() or 1))
+    os_ = ob.OracleSchema(cfg.chain)
+    keep = []
+    cols = ob.make_cols(hc, keep)
+    n = hc.n
+    total = ob.lib().or_encoded_size_one(ob.C.byref(os_.s), cols, 0, cfg.mode) * n \
+        if cfg.var_len is None else None
+    if total is None:
+        total = sum(ob.lib().or_encoded_size_one(ob.C.byref(os_.s), cols, i, cfg.mode) for i in range(n))
+    arena = np.empty(total, np.uint8)
+    offs = np.empty(n + 1, np.uint64)
+    res = {}
+    for label, th in (("mt", threads), ("st", 1)):
+        passes, t0 = 0, time.perf_counter()
+        budget = seconds if label == "mt" else seconds / 2
+        while True:
+            ob.lib().or_encode_batch(ob.C.byref(os_.s), cols, n, cfg.mode, arena.ctypes.data, arena.size,
+                                     offs.ctypes.data, None, th)
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                break
+        res[label] = (passes * n / el, passes, el, th)
+    return res
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from packos_amd.api import CompiledSchema, DeviceColumns, EncodePlan, encode_batch
+    from packos_amd.configs import CONFIGS, algorithmic_bytes, make_columns
+
+    cfg = CONFIGS[args.config]
+    n = args.n or (cfg.n // 8 if args.config == "C5" else cfg.n)
+    seed = cfg.seed + rank
+    hc = make_columns(cfg, n=n, seed=seed)
+    schema = CompiledSchema(cfg.chain, cfg.mode)
+    dcols = DeviceColumns.from_host(schema, hc, dev)
+    fixed = schema.fixed_blob_size > 0
+    stream = torch.cuda.current_stream()
+
+    # output buffers allocated once; for fixed-size schemas blob i is at i*B
+    r = encode_batch(schema, dcols, want_offsets=not fixed, want_status=False)
+    torch.cuda.synchronize()
+    total_out = r.total
+    out = r.arena
+
+    if fixed:
+        plan = EncodePlan(schema, dcols, out=out, stream=stream)
+        step = plan.run
+    else:
+        def step():
+            encode_batch(schema, dcols, want_offsets=True, want_status=False, out=out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    # dominant-kernel duration with HIP events on the launch stream
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    for a, b in evs:
+        a.record(stream)
+        step()
+        b.record(stream)
+    torch.cuda.synchronize()
+    kms = sorted(a.elapsed_time(b) for a, b in evs)
+    kernel_ms = float(np.mean(kms))
+    kernel_ms_med = float(np.median(kms))
+
+    alg = algorithmic_bytes(hc, total_out, with_offsets=not fixed)
+    blobs = n * args.steps * world
+    value = blobs / el / 1e6
+    achieved = alg / (kernel_ms * 1e-3) / 1e9
+
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                pmc = json.load(f)
+            traffic = pmc.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    e2e = None
+    if args.e2e and rank == 0:
+        e2e = e2e_rate(schema, cfg, hc, dev, fixed)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        nsamp = min(n, 1 << 20)
+        hs = make_columns(cfg, n=nsamp, seed=seed)
+        res = cpu_baseline(cfg, hs, args.cpu_seconds)
+        mt = res["mt"]
+        cpu = {"value": round(mt[0] / 1e6, 4), "unit": "million blobs/s", "cores": mt[3], "kind": "port",
+               "sample": f"{nsamp} blobs of config {args.config} (same generator, rank-0 seed), "
+                         f"{mt[1]} passes in {mt[2]:.1f} s; C restatement of PutAccess/Pack "
+                         f"(oracle/), {mt[3]} threads",
+               "single_thread_value": round(res['st'][0] / 1e6, 4)}
+
+    if rank == 0:
+        line = {
+            "metric": "million blobs/s + GiB/s device-resident encode, 1M×256B fixed-schema tuples",
+            "value": round(value, 3),
+            "unit": "million blobs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64, seed 0x%X + rank)" % cfg.seed,
+            "config": {"workload": f"{args.config}: {cfg.note}", "blobs_per_gpu": n,
+                       "blob_bytes": schema.fixed_blob_size if fixed else round(total_out / n, 1),
+                       "parallelism": f"dp{world} (independent shards, no collective)"},
+            "gib_per_s": round(total_out * args.steps * world / el / 2 ** 30, 2),
+            "kernel_ms": round(kernel_ms, 5),
+            "kernel_ms_median": round(kernel_ms_med, 5),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "algorithmic_bytes_per_launch": alg},
+            "cpu_baseline": cpu,
+        }
+        if e2e is not None:
+            line["e2e_pinned"] = e2e
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def e2e_rate(schema, cfg, hc, dev, fixed):
+    """Pinned host columns -> H2D -> encode -> D2H into pinned memory, chunked
+    and double-buffered on two streams (recorded in DESIGN.md, never `value`)."""
+    import torch
+    from packos_amd.api import DeviceColumns, encode_batch
+    n = hc.n
+    chunk = max(1, n // 8)
+    B = schema.fixed_blob_size
+    if not fixed:
+        return None
+    pin_cols = []
+    for c, sp in enumerate(schema.specs):
+        d = hc.data[c]
+        pin_cols.append(torch.from_numpy(d).pin_memory() if d is not None else None)
+    out_host = torch.empty(n * B, dtype=torch.uint8).pin_memory()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    bufs = []
+    for k in range(2):
+        cols = [None if p is None else torch.empty(chunk * sp.width, dtype=torch.uint8, device=dev)
+                for p, sp in zip(pin_cols, schema.specs)]
+        bufs.append((cols, torch.empty(chunk * B, dtype=torch.uint8, device=dev)))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j, s0 in enumerate(range(0, n, chunk)):
+        k = j % 2
+        m = min(chunk, n - s0)
+        st = streams[k]
+        cols, out = bufs[k]
+        with torch.cuda.stream(st):
+            for c, sp in enumerate(schema.specs):
+                if pin_cols[c] is not None:
+                    cols[c][: m * sp.width].copy_(pin_cols[c][s0 * sp.width:(s0 + m) * sp.width],
+                                                 non_blocking=True)
+            dc = DeviceColumns(schema, m, cols, [None] * len(cols), [None] * len(cols))
+            encode_batch(schema, dc, want_offsets=False, want_status=False, out=out, stream=st)
+            out_host[s0 * B:(s0 + m) * B].copy_(out[: m * B], non_blocking=True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"million_blobs_per_s": round(n / el / 1e6, 3), "gib_per_s_out": round(n * B / el / 2 ** 30, 3),
+            "chunks": (n + chunk - 1) // chunk, "note": "pinned H2D + encode + D2H, 2 streams"}
+
+
+if __name__ == "__main__":
+    main()

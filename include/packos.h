@@ -159,7 +159,8 @@ void packos_schema_free(packos_schema* s);
 int  packos_schema_num_columns(const packos_schema* s);
 int  packos_schema_num_top_fields(const packos_schema* s);
 int  packos_schema_column_info(const packos_schema* s, int col, packos_column_info* out);
-/* Blob size in bytes when every blob has the same size, else -1. */
+/* Blob size in bytes when the schema has no variable-width leaf and a call
+ * passes no validity columns (every nullable present), else -1.              */
 int64_t packos_schema_fixed_blob_size(const packos_schema* s);
 /* Host-side dump of the compiled layout program (debug/testing). Returns the
  * number of bytes needed (including NUL); writes at most cap bytes.          */
@@ -207,12 +208,15 @@ int packos_decode_batch(const packos_schema* s, const uint8_t* arena, const uint
 
 /* ---- random-access gather (GetAccess semantics) --------------------------- */
 
-/* For each blob walk `depth` positions (GetNestedGetAccess for all but the
- * last) and read the field at the last position:
+/* For each blob walk `depth` (<= 16) positions (GetNestedGetAccess for all
+ * but the last) and read the field at the last position.  `path` is HOST
+ * memory (copied into the launch); the outputs are device arrays:
  *   out_start[i]/out_len[i] = absolute [start,end) of the field payload,
  *   out_tag[i]  = its tag,
  *   status[i]   = 0 ok, 1 decode error (the Get* call would return an error
- *                 for `want_tag`/`want_width`), 2 nil nested access.
+ *                 for `want_tag`/`want_width`), 2 nil nested access (empty
+ *                 container), 3 nil accessor (NewGetAccess returned nil: the
+ *                 reference would dereference nil and panic).
  * want_width < 0 accepts any width >= 0 (GetBytes/GetString);
  * want_width == 0 is not used.                                               */
 int packos_get_field_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride,

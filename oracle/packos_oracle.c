@@ -418,12 +418,16 @@ int or_seq_peek(const or_seq* s, int* typ, int64_t* width) {
     *width = s->next_off - s->cur_off;
     return 0;
 }
+/* returns 0 ok, 1 "out of bounds" error, 2 = Go runtime panic: the header
+ * read binary.LittleEndian.Uint16(s.buf[(s.pos+1)*2:]) is not bounds
+ * checked (seqget.go:95) and panics when fewer than 2 bytes remain.         */
 int or_seq_advance(or_seq* s) {
     if (s->pos + 2 > s->count) return 1;
     s->pos++;
     s->cur_off = s->next_off;
     s->cur_type = s->next_type;
     if (s->cur_type != 0) {
+        if ((s->pos + 1) * 2 + 2 > s->len) return 2;
         uint16_t h = rd16(s->buf + (s->pos + 1) * 2);
         s->next_off = (h >> 3) + s->base;
         s->next_type = h & 7;
@@ -435,7 +439,7 @@ int or_seq_next(or_seq* s, int64_t* start, int64_t* width, int* typ) {
     if (or_seq_peek(s, typ, &w)) return 1;
     if (w < 0 || s->cur_off + w > s->len) return 1;
     *start = s->cur_off; *width = w;
-    return or_seq_advance(s);
+    return or_seq_advance(s) ? 1 : 0;
 }
 int or_seq_peek_nested(const or_seq* s, or_seq* nested) {
     if (s->cur_type != 7 && s->cur_type != 4) return 1;
@@ -448,11 +452,11 @@ int or_seq_peek_nested(const or_seq* s, or_seq* nested) {
 /* schema decode (schema/schema.go:893-910, 997-1052, 594-829, 270-326,      */
 /* 383-414, 1591-1633, 1062-1130 Match)                                       */
 /* ------------------------------------------------------------------------ */
-#define DEC_PANIC 0x100
-
 typedef struct dec_ctx {
     const or_schema* s; packos_column* cols; size_t i; uint64_t blob_base;
 } dec_ctx;
+
+#define DEC_PANIC 0x100
 
 /* precheck (schema.go:997-1013): 0 ok, else ErrConstraintViolated */
 static int precheck(const or_seq* q, int tag, int64_t hint, int nullable, int64_t* w) {
@@ -474,7 +478,9 @@ static int prim(or_seq* q, int tag, int64_t hint, int nullable, int64_t* ps, int
         if (q->cur_off + *w > q->len) return 1;
         *ps = q->cur_off;
     }
-    if (or_seq_advance(q)) return 2;
+    int a = or_seq_advance(q);
+    if (a == 2) return DEC_PANIC;
+    if (a) return 2;
     return 0;
 }
 
@@ -510,8 +516,9 @@ static int dec_node(dec_ctx* c, int n, or_seq* q, uint64_t sub_base) {
             return 0;
         }
         case ORN_MATCH: {
-            /* SString.Match(expected): CheckFunc DecodeFunc (schema.go:1092-1108) */
-            int e = prim(q, 6, 0, 1, &ps, &w);
+            /* SString.Match(expected): CheckFunc DecodeFunc (schema.go:1092-1108);
+             * the hint is the receiver SchemaString's Width (b)               */
+            int e = prim(q, 6, NB(s, n), NB(s, n) <= 0, &ps, &w);
             if (e) return e;
             size_t ll; const uint8_t* lp = lit_ptr(s, NA(s, n), &ll);
             size_t have = ps < 0 ? 0 : (size_t)w;
@@ -537,7 +544,9 @@ static int dec_node(dec_ctx* c, int n, or_seq* q, uint64_t sub_base) {
                 }
             }
             if (col && col->valid) col->valid[c->i] = w != 0;
-            if (or_seq_advance(q)) return 2;
+            int a = or_seq_advance(q);
+            if (a == 2) return DEC_PANIC;
+            if (a) return 2;
             return 0;
         }
     }

@@ -59,7 +59,7 @@ enum {
     ORN_BOOL = 4,   /* a = 1,     b = nullable                    SBool */
     ORN_STRING = 5, /* a = SchemaString.Width (0 nullable, >0 exact, -1 optional) */
     ORN_BYTES = 6,  /* a = SchemaBytes.Width */
-    ORN_MATCH = 7,  /* a = literal index (SString.Match / map key constant) */
+    ORN_MATCH = 7,  /* a = literal index, b = SchemaString Width (SString.Match / map key) */
     ORN_TUPLE = 8,  /* a = nullable, b = nchild, c = variableLength */
     ORN_MAP = 9     /* a = sorted,   b = nchild (key,value,...) */
 };

@@ -1,0 +1,284 @@
+"""Batch API over the C ABI: compile a schema once, then encode / decode whole
+batches of blobs resident in MI355X HBM.
+
+Reference correspondence (quickwritereader/PackOS):
+
+* ``CompiledSchema``      <- schema.BuildSchema + the Schema tree (schema/schema.go:177-182)
+* ``encode_batch``        <- PutAccess Add*/Pack() (access/put.go:69-308,619) per blob, or
+                             packable.Pack(args...) (packable/pack.go:59) with mode=MODE_PACKABLE
+* ``decode_batch``        <- schema.DecodeBuffer (schema/schema.go:893) per blob
+* ``get_field_batch``     <- GetAccess.Get*(pos) (access/get.go:60-375)
+
+Device memory is torch CUDA tensors (plumbing only); every byte of PackOS
+work happens in libpackos.so's HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import MODE_PACKABLE, MODE_PUTACCESS, PackosColumn, PackosColumnInfo, check, lib
+from .columns import HostColumns, column_specs
+from .schema import SchemaChain
+
+__all__ = ["CompiledSchema", "DeviceColumns", "DecodedColumns", "encode_batch", "decode_batch",
+           "get_field_batch", "MODE_PUTACCESS", "MODE_PACKABLE"]
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class CompiledSchema:
+    """A compiled, immutable schema handle (packos_schema*)."""
+
+    def __init__(self, chain, mode: int = MODE_PUTACCESS):
+        if isinstance(chain, SchemaChain):
+            self.chain = chain
+            js = json.dumps(chain.to_json())
+        else:
+            from .schema import BuildChain
+            js = chain if isinstance(chain, str) else json.dumps(chain)
+            self.chain = BuildChain(js)
+        self.mode = mode
+        self.json = js
+        h = C.c_void_p()
+        check(lib().packos_schema_compile(js.encode(), mode, C.byref(h)), "packos_schema_compile")
+        self._h = h
+        self.specs = column_specs(self.chain)
+        n = lib().packos_schema_num_columns(h)
+        assert n == len(self.specs), (n, len(self.specs))
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().packos_schema_free(h)
+            except Exception:
+                pass
+            self._h = None
+
+    @property
+    def n_columns(self) -> int:
+        return lib().packos_schema_num_columns(self._h)
+
+    def column_info(self, c: int) -> dict:
+        ci = PackosColumnInfo()
+        check(lib().packos_schema_column_info(self._h, c, C.byref(ci)), "column_info")
+        return {"kind": _lib.KIND_NAMES.get(ci.kind, "?"), "width": ci.width,
+                "nullable": bool(ci.nullable), "tag": ci.tag, "top_index": ci.top_index,
+                "depth": ci.depth, "name": ci.name.decode()}
+
+    @property
+    def fixed_blob_size(self) -> int:
+        return int(lib().packos_schema_fixed_blob_size(self._h))
+
+    def all_present_size(self) -> int:
+        return int(lib().packos_schema_blob_size_host(self._h, None, None))
+
+    def blob_size_host(self, widths: Optional[np.ndarray] = None,
+                       valid: Optional[np.ndarray] = None) -> int:
+        w = None if widths is None else np.ascontiguousarray(widths, np.uint32)
+        v = None if valid is None else np.ascontiguousarray(valid, np.uint8)
+        return int(lib().packos_schema_blob_size_host(
+            self._h, None if w is None else w.ctypes.data, None if v is None else v.ctypes.data))
+
+    def describe(self) -> str:
+        n = lib().packos_schema_describe(self._h, None, 0)
+        buf = C.create_string_buffer(n)
+        lib().packos_schema_describe(self._h, buf, n)
+        return buf.value.decode()
+
+
+class DeviceColumns:
+    """Input column set resident on a GPU (one entry per schema column)."""
+
+    def __init__(self, schema: CompiledSchema, n: int, data, offsets, valid):
+        self.schema = schema
+        self.n = int(n)
+        self.data: List = data
+        self.offsets: List = offsets
+        self.valid: List = valid
+
+    @classmethod
+    def from_host(cls, schema: CompiledSchema, hc: HostColumns, device="cuda"):
+        torch = _torch()
+        data, offs, valid = [], [], []
+        for c, sp in enumerate(schema.specs):
+            d = hc.data[c]
+            if d is not None:
+                t = torch.from_numpy(d if d.size else np.zeros(16, np.uint8)).to(device)
+                data.append(t)
+            else:
+                data.append(None)
+            o = hc.offsets[c]
+            offs.append(None if o is None else torch.from_numpy(o.view(np.int32)).to(device))
+            v = hc.valid[c]
+            valid.append(None if v is None else torch.from_numpy(v).to(device))
+        return cls(schema, hc.n, data, offs, valid)
+
+    def any_valid(self) -> bool:
+        return any(v is not None for v in self.valid)
+
+    def has_var(self) -> bool:
+        return any(sp.var for sp in self.schema.specs)
+
+    def ctypes_array(self):
+        arr = (PackosColumn * max(1, len(self.schema.specs)))()
+        for c in range(len(self.schema.specs)):
+            arr[c].data = self.data[c].data_ptr() if self.data[c] is not None else None
+            arr[c].offsets = self.offsets[c].data_ptr() if self.offsets[c] is not None else None
+            arr[c].valid = self.valid[c].data_ptr() if self.valid[c] is not None else None
+        return arr
+
+    def nbytes(self) -> int:
+        t = 0
+        for lst in (self.data, self.offsets, self.valid):
+            for x in lst:
+                if x is not None:
+                    t += x.numel() * x.element_size()
+        return t
+
+
+def _stream_ptr(stream):
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+@dataclass
+class EncodeResult:
+    arena: object      # torch.uint8 [total]
+    offsets: object    # torch.int64 [n+1] or None (fixed size: blob i at i*B)
+    status: object     # torch.int32 [n] or None
+    total: int
+    blob_size: int     # B for fixed-size batches, -1 otherwise
+
+
+def encode_batch(schema: CompiledSchema, cols: DeviceColumns, want_offsets: bool = True,
+                 want_status: bool = True, out=None, stream=None) -> EncodeResult:
+    """Encode every blob of the batch (async on `stream`; one host sync for
+    variable-size batches to size the arena)."""
+    torch = _torch()
+    L = lib()
+    n = cols.n
+    dev = cols.data[0].device if cols.data and cols.data[0] is not None else torch.device("cuda")
+    st = _stream_ptr(stream)
+    arr = cols.ctypes_array()
+    status = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if want_status else None
+    fixed = (not cols.has_var()) and not cols.any_valid()
+    if fixed:
+        B = schema.all_present_size()
+        total = B * n
+        if out is None:
+            out = torch.empty(max(total, 16), dtype=torch.uint8, device=dev)
+        offs = torch.empty(n + 1, dtype=torch.int64, device=dev) if want_offsets else None
+        check(L.packos_encode_batch(schema.handle, arr, n, out.data_ptr(), out.numel(),
+                                    None if offs is None else offs.data_ptr(),
+                                    None if status is None else status.data_ptr(), None, 0, 0, st),
+              "packos_encode_batch")
+        return EncodeResult(out, offs, status[:n] if status is not None else None, total, B)
+    offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    wsb = L.packos_encode_workspace_size(schema.handle, n)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    check(L.packos_encoded_size_batch(schema.handle, arr, n, offs.data_ptr(), ws.data_ptr(), wsb, st),
+          "packos_encoded_size_batch")
+    total = int(offs[n].item()) if n else 0
+    if out is None or out.numel() < total:
+        out = torch.empty(max(total, 16), dtype=torch.uint8, device=dev)
+    check(L.packos_encode_batch(schema.handle, arr, n, out.data_ptr(), out.numel(), offs.data_ptr(),
+                                None if status is None else status.data_ptr(), ws.data_ptr(), wsb,
+                                _lib.ENC_OFFSETS_READY, st), "packos_encode_batch")
+    return EncodeResult(out, offs, status[:n] if status is not None else None, total, -1)
+
+
+class EncodePlan:
+    """Pre-bound encode of a fixed-size batch into a preallocated arena: one
+    C-ABI call per run() (what a serving loop or graph capture replays)."""
+
+    def __init__(self, schema: CompiledSchema, cols: DeviceColumns, out=None, stream=None):
+        torch = _torch()
+        if cols.has_var() or cols.any_valid():
+            raise ValueError("EncodePlan is for fixed-size batches")
+        self.schema, self.cols = schema, cols
+        self.B = schema.all_present_size()
+        self.total = self.B * cols.n
+        dev = cols.data[0].device
+        self.out = out if out is not None else torch.empty(max(self.total, 16), dtype=torch.uint8, device=dev)
+        self._arr = cols.ctypes_array()
+        self._stream = stream
+        self._args = None
+
+    def run(self):
+        st = _stream_ptr(self._stream)
+        check(lib().packos_encode_batch(self.schema.handle, self._arr, self.cols.n, self.out.data_ptr(),
+                                        self.out.numel(), None, None, None, 0, 0, st), "packos_encode_batch")
+        return self.out
+
+
+class DecodedColumns:
+    """Decode output: fixed columns, validity, (start, length) views of var
+    columns into the input arena."""
+
+    def __init__(self, schema: CompiledSchema, n: int, device):
+        torch = _torch()
+        self.schema, self.n = schema, n
+        self.data, self.valid, self.start, self.length = [], [], [], []
+        for sp in schema.specs:
+            self.data.append(torch.zeros(max(n * sp.width, 16), dtype=torch.uint8, device=device)
+                             if sp.fixed else None)
+            self.valid.append(torch.full((max(n, 1),), 255, dtype=torch.uint8, device=device)
+                              if sp.has_valid else None)
+            self.start.append(torch.zeros(max(n, 1), dtype=torch.int64, device=device) if sp.var else None)
+            self.length.append(torch.zeros(max(n, 1), dtype=torch.int32, device=device) if sp.var else None)
+
+    def ctypes_array(self):
+        arr = (PackosColumn * max(1, len(self.schema.specs)))()
+        for c in range(len(self.schema.specs)):
+            arr[c].data = self.data[c].data_ptr() if self.data[c] is not None else None
+            arr[c].valid = self.valid[c].data_ptr() if self.valid[c] is not None else None
+            arr[c].start = self.start[c].data_ptr() if self.start[c] is not None else None
+            arr[c].length = self.length[c].data_ptr() if self.length[c] is not None else None
+        return arr
+
+
+def decode_batch(schema: CompiledSchema, arena, offsets=None, n: Optional[int] = None, stride: int = 0,
+                 stream=None):
+    """schema.DecodeBuffer over every blob; returns (DecodedColumns, status)."""
+    torch = _torch()
+    if n is None:
+        n = offsets.numel() - 1
+    out = DecodedColumns(schema, n, arena.device)
+    status = torch.empty(max(n, 1), dtype=torch.int32, device=arena.device)
+    check(lib().packos_decode_batch(schema.handle, arena.data_ptr(),
+                                    None if offsets is None else offsets.data_ptr(), stride, n,
+                                    out.ctypes_array(), status.data_ptr(), _stream_ptr(stream)),
+          "packos_decode_batch")
+    return out, status[:n]
+
+
+def get_field_batch(arena, offsets, n: int, path, want_tag: int, want_width: int, stride: int = 0,
+                    stream=None):
+    """GetAccess.Get*(path) over every blob: (start, length, tag, status)."""
+    torch = _torch()
+    dev = arena.device
+    s0 = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    ln = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    tg = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    st = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    p = (C.c_int32 * len(path))(*path)
+    check(lib().packos_get_field_batch(arena.data_ptr(), None if offsets is None else offsets.data_ptr(),
+                                       stride, n, p, len(path), want_tag, want_width, s0.data_ptr(),
+                                       ln.data_ptr(), tg.data_ptr(), st.data_ptr(), _stream_ptr(stream)),
+          "packos_get_field_batch")
+    return s0[:n], ln[:n], tg[:n], st[:n]

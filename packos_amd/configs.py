@@ -1,0 +1,150 @@
+"""BASELINE.json configurations and their synthetic inputs.
+
+Every value comes from a splitmix64 stream (seeded per config / column) so the
+GPU path and the CPU oracle see identical inputs:
+
+* ints uniform over the full range, float64 = raw random 64-bit patterns
+  (NaN payloads included; encode copies bits, access/put.go:130-134),
+  bool = bit 0, string bytes printable ASCII 0x20-0x7E, bytes uniform.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Dict, Optional
+
+import numpy as np
+
+from .columns import HostColumns, column_specs
+from .schema import (SBool, SBytes, SFloat64, SInt16, SInt32, SInt64, SMapSorted, SString,
+                     SStringLen, SVariableBytes, SVariableString, SchemaChain, SchemaNamedChain,
+                     SChain)
+
+GOLDEN_GAMMA = np.uint64(0x9E3779B97F4A7C15)
+
+
+def splitmix64(seed: int, count: int) -> np.ndarray:
+    """splitmix64 outputs z_1..z_count for state `seed` (state += gamma first)."""
+    with np.errstate(over="ignore"):
+        k = np.arange(1, count + 1, dtype=np.uint64)
+        z = np.uint64(seed) + k * GOLDEN_GAMMA
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z
+
+
+def random_bytes(seed: int, nbytes: int) -> np.ndarray:
+    words = splitmix64(seed, (nbytes + 7) // 8)
+    return words.view(np.uint8)[:nbytes].copy()
+
+
+def _col_seed(seed: int, c: int) -> int:
+    return (seed + (c + 1) * 0x1000_0000_0000) & 0xFFFF_FFFF_FFFF_FFFF
+
+
+@dataclass
+class Config:
+    name: str
+    chain: SchemaChain
+    n: int
+    seed: int
+    mode: int = 0
+    var_len: Optional[Callable] = None   # (n, seed) -> dict col -> lengths
+    note: str = ""
+
+
+def fixed_columns(chain: SchemaChain, n: int, seed: int, var_lengths: Optional[Dict[int, np.ndarray]] = None
+                  ) -> HostColumns:
+    """Synthetic HostColumns for any schema (no nils)."""
+    hc = HostColumns(chain, n)
+    for c, sp in enumerate(hc.specs):
+        node = sp.node
+        s = _col_seed(seed, c)
+        if sp.fixed:
+            raw = random_bytes(s, n * sp.width)
+            if node.kind == "bool":
+                raw &= 1
+            elif node.kind == "string":
+                raw = (0x20 + (raw % 95)).astype(np.uint8)
+            hc.data[c] = raw
+        elif sp.var:
+            lens = var_lengths[c] if var_lengths and c in var_lengths else np.zeros(n, np.uint32)
+            lens = np.asarray(lens, dtype=np.uint64)
+            offs = np.zeros(n + 1, dtype=np.uint64)
+            np.cumsum(lens, out=offs[1:])
+            if offs[-1] >= 2 ** 32:
+                raise ValueError("var column arena exceeds uint32 offsets; shard the batch")
+            raw = random_bytes(s, int(offs[-1]))
+            if node.kind == "string":
+                raw = (0x20 + (raw % 95)).astype(np.uint8)
+            hc.data[c] = raw
+            hc.offsets[c] = offs.astype(np.uint32)
+        elif sp.has_valid:
+            hc.valid[c] = None  # containers always present in the configs
+    return hc
+
+
+# ---- schemas -------------------------------------------------------------------
+# Metric M: 1M x 256 B fixed-schema tuples (8 fields, H = 18, payload 238)
+CHAIN_M = SChain(SInt16, SInt32, SInt64, SFloat64, SBool, SStringLen(96), SStringLen(64), SBytes(55))
+# C1: README template (int16, bool, string[2], bytes[2]) -> 17 B
+CHAIN_C1 = SChain(SInt16, SBool, SStringLen(2), SBytes(2))
+# C2: put_bench primitives subset: int16, int64, bool, string[24], bytes[17] -> 64 B
+CHAIN_C2 = SChain(SInt16, SInt64, SBool, SStringLen(24), SBytes(17))
+# C3: schema-guided named chain (names stripped on the wire)
+CHAIN_C3 = SchemaNamedChain((SInt32, SInt64, SFloat64, SBool, SString, SStringLen(8), SBytes(16)),
+                            ("id", "ts", "score", "flag", "label", "code", "digest"))
+# C4: outer tuple with one nested PackMapSorted{kid1,kid2,role,user -> string[24]} -> 256 B
+CHAIN_C4 = SChain(SInt16, SInt64, SBool, SStringLen(103),
+                  SMapSorted(SString.Match("user"), SStringLen(24), SString.Match("role"), SStringLen(24),
+                             SString.Match("kid2"), SStringLen(24), SString.Match("kid1"), SStringLen(24)))
+# C5: mixed 64 B - 4 KB blobs
+CHAIN_C5 = SChain(SInt16, SInt64, SBool, SVariableString(), SVariableBytes())
+
+
+def c3_lengths(n: int, seed: int) -> Dict[int, np.ndarray]:
+    r = splitmix64(seed ^ 0xC3C3, n)
+    return {4: (8 + (r % np.uint64(33))).astype(np.uint32)}  # column 4 = SString, 8..40 B
+
+
+def c5_lengths(n: int, seed: int) -> Dict[int, np.ndarray]:
+    """Blob size log-uniform in [64, 4096]: B = 12 (H) + 11 + ls + lb."""
+    r = splitmix64(seed ^ 0xC5C5, n).astype(np.float64) / 2.0 ** 64
+    B = np.floor(np.exp(np.log(64.0) + r * (np.log(4096.0) - np.log(64.0)))).astype(np.int64)
+    B = np.clip(B, 64, 4096)
+    rest = B - 23
+    ls = rest // 2
+    lb = rest - ls
+    return {3: ls.astype(np.uint32), 4: lb.astype(np.uint32)}
+
+
+CONFIGS = {
+    "M": Config("M", CHAIN_M, 1 << 20, 0x5EED0001,
+                note="1M x 256 B fixed-schema tuples (metric)"),
+    "C1": Config("C1", CHAIN_C1, 1000, 0x5EED0000, note="1k flat (int16,bool,string[2],bytes[2])"),
+    "C2": Config("C2", CHAIN_C2, 1 << 20, 0x5EED0002, note="1M x 64 B PutAccess primitives"),
+    "C3": Config("C3", CHAIN_C3, 1 << 20, 0x5EED0003, var_len=c3_lengths,
+                 note="1M schema-guided records, encode+decode"),
+    "C4": Config("C4", CHAIN_C4, 4 << 20, 0x5EED0004, note="4M x 256 B with nested PackMapSorted"),
+    "C5": Config("C5", CHAIN_C5, 64 << 20, 0x5EED0005, var_len=c5_lengths,
+                 note="64M mixed 64 B-4 KB across 8 GPUs (per-shard seed + shard)"),
+}
+
+
+def make_columns(cfg: Config, n: Optional[int] = None, seed: Optional[int] = None) -> HostColumns:
+    n = cfg.n if n is None else n
+    seed = cfg.seed if seed is None else seed
+    vl = cfg.var_len(n, seed) if cfg.var_len else None
+    return fixed_columns(cfg.chain, n, seed, vl)
+
+
+def algorithmic_bytes(hc: HostColumns, total_out: int, with_offsets: bool) -> int:
+    """bytes_in + bytes_out: value bytes + 4 B/var offset read,
+    blob bytes written (+8 B per blob offset when emitted)."""
+    tin = 0
+    for c, sp in enumerate(hc.specs):
+        if sp.fixed:
+            tin += hc.n * sp.width
+        elif sp.var:
+            tin += int(hc.offsets[c][-1]) + 4 * hc.n
+    return tin + total_out + (8 * hc.n if with_offsets else 0)

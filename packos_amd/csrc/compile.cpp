@@ -1,0 +1,645 @@
+// compile.cpp — host schema compiler: SchemaJSON -> encode / fixed-layout /
+// decode programs.  No GPU needed.
+//
+// Replaces schema.BuildSchema (schema/schemabuilder_json.go:124-300) for the
+// fixed-schema subset and resolves, once per schema, everything the reference
+// recomputes per blob: map key order (utils.SortKeys, utils/utils.go:7-14),
+// header-block sizes (access/put.go:619-627, packable/pack.go:36) and, for
+// fixed-size schemas, every header word of the blob.
+#include <algorithm>
+#include <cstring>
+#include <sstream>
+
+#include "json_lite.hpp"
+#include "schema_impl.h"
+
+using namespace packos;
+
+namespace {
+
+thread_local std::string g_err;
+
+struct CompileError {
+    int code;
+    std::string msg;
+};
+
+[[noreturn]] void fail(int code, const std::string& m) { throw CompileError{code, m}; }
+
+int tag_of(int kind) {
+    switch (kind) {
+        case K_INT: case K_UINT: return PACKOS_TAG_INTEGER;
+        case K_FLOAT: return PACKOS_TAG_FLOATING;
+        case K_BOOL: return PACKOS_TAG_BOOL;
+        case K_STRING: case K_BYTES: case K_MATCH: return PACKOS_TAG_STRING;
+        case K_TUPLE: return PACKOS_TAG_TUPLE;
+        case K_MAP: return PACKOS_TAG_MAP;
+    }
+    return 0;
+}
+
+// uint16(offset<<3) | tag (typetags/types.go:44-46): silently truncating
+uint16_t enc_header(int64_t off, int tag) { return (uint16_t)((((uint64_t)off) << 3) & 0xFFFFu) | (uint16_t)(tag & 7); }
+
+struct Builder {
+    packos_schema* s;
+
+    int new_node() {
+        s->nodes.emplace_back();
+        return (int)s->nodes.size() - 1;
+    }
+
+    static int width_of(const char* t) {
+        if (!strcmp(t, "8")) return 1;
+        if (!strcmp(t, "16")) return 2;
+        if (!strcmp(t, "32")) return 4;
+        if (!strcmp(t, "64")) return 8;
+        return 0;
+    }
+
+    static std::string str_field(const JVal& j, const char* k) {
+        const JVal* v = j.get(k);
+        return (v && v->kind == JVal::STR) ? v->str : std::string();
+    }
+    static bool bool_field(const JVal& j, const char* k, bool dflt = false) {
+        const JVal* v = j.get(k);
+        return v ? v->truthy() : dflt;
+    }
+    static int int_field(const JVal& j, const char* k) {
+        const JVal* v = j.get(k);
+        return (v && v->kind == JVal::NUM) ? (int)v->num : 0;
+    }
+
+    // BuildSchema (schemabuilder_json.go:124-300), compiled subset
+    int node(const JVal& j, int parent, int depth, int top, const std::string& name) {
+        if (j.kind != JVal::OBJ) fail(PACKOS_E_SCHEMA, "schema node must be an object");
+        if (depth >= kMaxDepth - 1) fail(PACKOS_E_UNSUPPORTED, "nesting deeper than supported");
+        std::string t = str_field(j, "type");
+        int id = new_node();
+        {
+            Node& n = s->nodes[id];
+            n.parent = parent;
+            n.depth = depth;
+            n.top = top;
+            n.name = name;
+        }
+        bool nullable = bool_field(j, "nullable");
+        auto unsupported_keys = [&](std::initializer_list<const char*> keys) {
+            for (const char* k : keys)
+                if (j.get(k) && !(j.get(k)->kind == JVal::STR && j.get(k)->str.empty()))
+                    fail(PACKOS_E_UNSUPPORTED, std::string("'") + k + "' on a " + t +
+                                                   " node is outside the compiled subset");
+        };
+        if (t == "bool") {
+            Node& n = s->nodes[id];
+            n.kind = K_BOOL; n.width = 1; n.nullable = nullable;
+        } else if (t.rfind("int", 0) == 0 && width_of(t.c_str() + 3)) {
+            unsupported_keys({"min", "max"});
+            Node& n = s->nodes[id];
+            n.kind = K_INT; n.width = width_of(t.c_str() + 3); n.nullable = nullable;
+        } else if (t.rfind("uint", 0) == 0 && width_of(t.c_str() + 4)) {
+            Node& n = s->nodes[id];
+            n.kind = K_UINT; n.width = width_of(t.c_str() + 4); n.nullable = nullable;
+        } else if (t == "float32" || t == "float64") {
+            Node& n = s->nodes[id];
+            n.kind = K_FLOAT; n.width = t == "float32" ? 4 : 8; n.nullable = nullable;
+        } else if (t == "string") {
+            unsupported_keys({"prefix", "suffix", "pattern", "decodeDefault"});
+            // SString / Optional() (Width -1) / WithWidth(n) (schemabuilder_json.go:184-208)
+            int w = 0;
+            if (nullable) w = -1;
+            else if (int_field(j, "width") > 0) w = int_field(j, "width");
+            Node& n = s->nodes[id];
+            n.width = w;
+            n.nullable = w <= 0;
+            if (j.get("exact") && !str_field(j, "exact").empty()) {
+                n.kind = K_MATCH;
+                n.literal = str_field(j, "exact");
+            } else {
+                n.kind = K_STRING;
+            }
+        } else if (t == "bytes") {
+            int w = int_field(j, "width");
+            Node& n = s->nodes[id];
+            n.kind = K_BYTES; n.width = w > 0 ? w : -1; n.nullable = n.width <= 0;
+        } else if (t == "tuple") {
+            if (bool_field(j, "flatten")) fail(PACKOS_E_UNSUPPORTED, "flattened tuples are outside the compiled subset");
+            const JVal* sch = j.get("schema");
+            const JVal* names = j.get("fieldNames");
+            {
+                Node& n = s->nodes[id];
+                n.kind = K_TUPLE;
+                n.nullable = bool_field(j, "nullable", true);  // STuple* are Nullable: true
+                n.variable = bool_field(j, "variableLength");
+            }
+            if (sch && sch->kind == JVal::ARR) {
+                for (size_t k = 0; k < sch->arr.size(); k++) {
+                    std::string nm;
+                    if (names && names->kind == JVal::ARR && k < names->arr.size() &&
+                        names->arr[k].kind == JVal::STR)
+                        nm = names->arr[k].str;
+                    std::string path = name.empty() ? nm : (nm.empty() ? name : name + "." + nm);
+                    int kid = node(sch->arr[k], id, depth + 1, top, path);
+                    s->nodes[id].kids.push_back(kid);
+                }
+            }
+        } else if (t == "map") {
+            const JVal* sch = j.get("schema");
+            {
+                Node& n = s->nodes[id];
+                n.kind = K_MAP;
+                n.width = -1;
+                n.nullable = true;  // SchemaMap.IsNullable: Width <= 0
+                n.sorted = bool_field(j, "sorted");
+            }
+            if (sch && sch->kind == JVal::ARR) {
+                if (sch->arr.size() % 2)
+                    fail(PACKOS_E_SCHEMA, "map schema needs key,value pairs (schema.go:395-403)");
+                for (size_t k = 0; k < sch->arr.size(); k++) {
+                    int kid = node(sch->arr[k], id, depth + 1, top, name);
+                    int kk = s->nodes[kid].kind;
+                    if (k % 2 == 0 && kk != K_MATCH && kk != K_STRING)
+                        fail(PACKOS_E_SCHEMA, "map keys must be strings");
+                    s->nodes[id].kids.push_back(kid);
+                }
+            }
+            Node& n = s->nodes[id];
+            if (n.sorted) {
+                size_t np = n.kids.size() / 2;
+                std::vector<std::pair<int, int>> pairs;
+                for (size_t p = 0; p < np; p++) {
+                    if (s->nodes[n.kids[2 * p]].kind != K_MATCH)
+                        fail(PACKOS_E_SCHEMA, "sorted maps need exact (constant) keys");
+                    pairs.emplace_back(n.kids[2 * p], n.kids[2 * p + 1]);
+                }
+                // sort.Strings order = bytewise (utils/utils.go:7-14)
+                std::stable_sort(pairs.begin(), pairs.end(), [&](auto& a, auto& b) {
+                    return s->nodes[a.first].literal < s->nodes[b.first].literal;
+                });
+                std::vector<int> k2;
+                for (auto& p : pairs) { k2.push_back(p.first); k2.push_back(p.second); }
+                n.kids = k2;
+            }
+        } else {
+            fail(PACKOS_E_UNSUPPORTED, "schema type '" + t + "' is outside the compiled subset");
+        }
+        return id;
+    }
+
+    void assign_columns(int id) {
+        Node& n = s->nodes[id];
+        if (n.kind != K_MATCH && n.kind != K_ROOT) {
+            n.col = (int)s->col_node.size();
+            s->col_node.push_back(id);
+        }
+        for (int k : s->nodes[id].kids) assign_columns(k);
+    }
+
+    // ---------------------------------------------------------- encode ----
+    int emit_container(int id, int cont_id) {
+        Node& n = s->nodes[id];
+        int nk = (int)n.kids.size();
+        EncItem hdr{};
+        hdr.type = IT_HDR;
+        hdr.cont = (int16_t)cont_id;
+        hdr.col = -1;
+        hdr.size = nk ? (uint32_t)(2 * (nk + 1)) : (s->mode == PACKOS_MODE_PUTACCESS ? 2u : 0u);
+        int hdr_item = (int)s->items.size();
+        s->items.push_back(hdr);
+        s->conts[cont_id].hdr_item = (uint16_t)hdr_item;
+        s->conts[cont_id].n_kids = (uint16_t)nk;
+        std::vector<int> kid_start;
+        for (int k : n.kids) {
+            kid_start.push_back((int)s->items.size());
+            emit_node(k, cont_id);
+        }
+        int end_item = (int)s->items.size();
+        if (nk == 0) {
+            if (s->mode == PACKOS_MODE_PUTACCESS) {
+                // BeginX/EndNested (or Pack() of an empty accessor) appends End(0)
+                // and rewrites h0 as EncodeHeader(2, 0) = 0x0010 (put.go:619-652)
+                EncHdr h{};
+                h.hdr_item = (uint16_t)hdr_item; h.cont = (uint16_t)cont_id;
+                h.relative = 0; h.j = 0; h.value = enc_header(2, 0); h.tag = 0;
+                s->hdrs.push_back(h);
+            }
+            return end_item;
+        }
+        for (int j = 0; j <= nk; j++) {
+            EncHdr h{};
+            h.hdr_item = (uint16_t)hdr_item;
+            h.cont = (uint16_t)cont_id;
+            h.j = (uint16_t)j;
+            if (j == 0) {
+                int64_t hs = 2 * (int64_t)(nk + 1);
+                h.relative = 0;
+                h.tag = (uint8_t)tag_of(s->nodes[n.kids[0]].kind);
+                h.value = enc_header(hs, h.tag);
+                h.ovf = hs >= 8192;
+            } else if (j < nk) {
+                h.relative = 1;
+                h.target = (uint16_t)kid_start[j];
+                h.tag = (uint8_t)tag_of(s->nodes[n.kids[j]].kind);
+            } else {
+                h.relative = 1;
+                h.target = (uint16_t)end_item;
+                h.tag = 0;
+            }
+            s->hdrs.push_back(h);
+        }
+        return end_item;
+    }
+
+    void emit_node(int id, int cont_id) {
+        Node& n = s->nodes[id];
+        EncItem it{};
+        it.cont = (int16_t)cont_id;
+        it.col = (int16_t)n.col;
+        switch (n.kind) {
+            case K_INT: case K_UINT: case K_FLOAT: case K_BOOL:
+                it.type = IT_FIXED;
+                it.size = (uint32_t)n.width;
+                it.nullable = n.nullable;
+                it.is_bool = n.kind == K_BOOL;
+                s->items.push_back(it);
+                if (n.nullable) s->has_nullable = true;
+                return;
+            case K_STRING: case K_BYTES:
+                if (n.width > 0) {
+                    it.type = IT_FIXED;
+                    it.size = (uint32_t)n.width;
+                } else {
+                    it.type = IT_VAR;
+                    s->has_var = true;
+                }
+                s->items.push_back(it);
+                return;
+            case K_MATCH:
+                it.type = IT_CONST;
+                it.col = -1;
+                it.size = (uint32_t)n.literal.size();
+                it.lit = (uint32_t)s->lits.size();
+                s->lits.insert(s->lits.end(), n.literal.begin(), n.literal.end());
+                s->items.push_back(it);
+                return;
+            case K_TUPLE: case K_MAP: {
+                if ((int)s->conts.size() >= kMaxConts) fail(PACKOS_E_UNSUPPORTED, "too many nested containers");
+                EncCont c{};
+                c.parent = (int16_t)cont_id;
+                bool can_nil = n.kind == K_MAP || n.nullable;
+                c.valid_col = can_nil ? (int16_t)n.col : (int16_t)-1;
+                if (can_nil) s->has_nullable = true;
+                int cid = (int)s->conts.size();
+                s->conts.push_back(c);
+                emit_container(id, cid);
+                return;
+            }
+        }
+        fail(PACKOS_E_SCHEMA, "bad node");
+    }
+
+    void build_encode() {
+        s->items.clear(); s->hdrs.clear(); s->conts.clear(); s->lits.clear();
+        EncCont root{};
+        root.parent = -1;
+        root.valid_col = -1;
+        s->conts.push_back(root);
+        if (s->mode == PACKOS_MODE_PACKABLE && s->nodes[0].kids.empty()) {
+            // packable.Pack() with no args: empty slice (pack.go:59-67)
+            s->conts[0].hdr_item = 0;
+            return;
+        }
+        emit_container(0, 0);
+        if (s->items.size() > 65000) fail(PACKOS_E_UNSUPPORTED, "schema too large");
+    }
+
+    // All-present blob layout for schemas without var leaves.
+    void build_fixed() {
+        s->fix_ok = false;
+        s->all_present_size = -1;
+        if (s->has_var) return;
+        size_t ni = s->items.size();
+        std::vector<int64_t> pos(ni + 1, 0);
+        for (size_t i = 0; i < ni; i++) pos[i + 1] = pos[i] + s->items[i].size;
+        int64_t B = pos[ni];
+        s->all_present_size = B;
+        // byte map: -1 const, else (col, off) packed
+        struct BM { int col; int off; uint8_t val; bool is_bool; };
+        std::vector<BM> bm((size_t)B, BM{-1, 0, 0, false});
+        bool ovf = false;
+        for (size_t i = 0; i < ni; i++) {
+            const EncItem& it = s->items[i];
+            if (it.type == IT_CONST)
+                for (uint32_t k = 0; k < it.size; k++) bm[pos[i] + k].val = s->lits[it.lit + k];
+            else if (it.type == IT_FIXED)
+                for (uint32_t k = 0; k < it.size; k++) bm[pos[i] + k] = BM{it.col, (int)k, 0, it.is_bool != 0};
+        }
+        for (const EncHdr& h : s->hdrs) {
+            const EncItem& hi = s->items[h.hdr_item];
+            int64_t payload = pos[h.hdr_item] + hi.size;
+            uint16_t v;
+            if (h.relative) {
+                int64_t off = pos[h.target] - payload;
+                if (off >= 8192) ovf = true;
+                v = enc_header(off, h.tag);
+            } else {
+                v = h.value;
+                if (h.ovf) ovf = true;
+            }
+            int64_t at = pos[h.hdr_item] + 2 * h.j;
+            bm[at].val = (uint8_t)(v & 0xFF);
+            bm[at + 1].val = (uint8_t)(v >> 8);
+        }
+        s->all_present_overflow = ovf;
+        if (B <= 0 || B > 1024) return;  // large fixed blobs use the general kernel
+
+        // tile size: T blobs (multiple of 16 so tile in/out are whole 16-B chunks)
+        int T = (int)((16384 / B) / 16 * 16);
+        if (T < 16) T = 16;
+        if (T > 1024) T = 1024;
+        s->fix_T = T;
+        // LDS regions per fixed column (16-B guards on both sides)
+        s->fcols.clear();
+        std::vector<int> lds_of_col(s->col_node.size(), -1);
+        uint32_t lds = 16, chunks = 0;
+        for (size_t c = 0; c < s->col_node.size(); c++) {
+            const Node& n = s->nodes[s->col_node[c]];
+            bool fixed_leaf = (n.kind >= K_INT && n.kind <= K_BOOL) ||
+                              ((n.kind == K_STRING || n.kind == K_BYTES) && n.width > 0);
+            if (!fixed_leaf) continue;
+            FixCol fc{};
+            fc.col = (int)c;
+            fc.width = (uint32_t)n.width;
+            fc.lds_off = lds;
+            fc.chunk_begin = chunks;
+            lds_of_col[c] = (int)lds;
+            uint32_t bytes = (uint32_t)T * fc.width;
+            chunks += bytes / 16;
+            lds += bytes + 32;  // region + guard (next region's leading guard)
+            lds = (lds + 15) & ~15u;
+            s->fcols.push_back(fc);
+        }
+        s->fix_lds = (int)lds + 16;
+        s->fix_chunks = (int)chunks;
+        if (s->fix_lds > 60 * 1024) return;
+        // segments for each dword r of a 4-blob period
+        s->fsegs.clear();
+        s->fseg_index.assign((size_t)B + 1, 0);
+        for (int64_t r = 0; r < B; r++) {
+            s->fseg_index[r] = (uint32_t)s->fsegs.size();
+            uint32_t cmask = 0, cval = 0;
+            int b = 0;
+            while (b < 4) {
+                int64_t pb = 4 * r + b;
+                int d = (int)(pb / B);
+                int64_t q = pb % B;
+                const BM& m = bm[q];
+                if (m.col < 0) {
+                    cmask |= 0xFFu << (8 * b);
+                    cval |= (uint32_t)m.val << (8 * b);
+                    b++;
+                    continue;
+                }
+                // extend the run: same column, same blob, consecutive source bytes
+                int b1 = b + 1;
+                while (b1 < 4) {
+                    int64_t pb1 = 4 * r + b1;
+                    int d1 = (int)(pb1 / B);
+                    const BM& m1 = bm[pb1 % B];
+                    if (m1.col != m.col || d1 != d || m1.off != m.off + (b1 - b) || m.is_bool) break;
+                    b1++;
+                }
+                FixSeg sg{};
+                uint32_t w = (uint32_t)s->nodes[s->col_node[m.col]].width;
+                sg.a = lds_of_col[m.col] + d * (int)w + m.off - b;
+                sg.stride4 = 4 * w;
+                uint32_t mask = 0;
+                for (int x = b; x < b1; x++) mask |= 0xFFu << (8 * x);
+                sg.mask = mask;
+                sg.cval = m.is_bool ? 1u : 0u;
+                s->fsegs.push_back(sg);
+                b = b1;
+            }
+            if (cmask) {
+                FixSeg sg{};
+                sg.a = 0; sg.stride4 = 0; sg.mask = cmask; sg.cval = cval;
+                s->fsegs.push_back(sg);
+            }
+        }
+        s->fseg_index[B] = (uint32_t)s->fsegs.size();
+        // tile + descriptor tables must fit the 64 KiB dynamic LDS of one launch
+        size_t lds_total = (size_t)s->fix_lds + ((size_t)(B + 1) * 4 + 15) / 16 * 16 + s->fsegs.size() * sizeof(FixSeg);
+        s->fix_ok = lds_total <= 64 * 1024;
+    }
+
+    // ---------------------------------------------------------- decode ----
+    void build_decode() {
+        s->dnodes.assign(s->nodes.size(), DecNode{});
+        s->dkids.clear();
+        for (size_t i = 0; i < s->nodes.size(); i++) {
+            const Node& n = s->nodes[i];
+            DecNode& d = s->dnodes[i];
+            d.kind = n.kind;
+            d.width = n.width;
+            d.col = n.col;
+            d.nkids = (int)n.kids.size();
+            d.kid0 = (int)s->dkids.size();
+            for (int k : n.kids) s->dkids.push_back(k);
+            d.tag = (uint8_t)tag_of(n.kind);
+            d.variable = n.variable;
+            switch (n.kind) {
+                case K_STRING: case K_BYTES: case K_MATCH: d.nullable = n.width <= 0; break;
+                case K_MAP: d.nullable = 1; break;
+                default: d.nullable = n.nullable;
+            }
+            if (n.kind == K_MATCH) {
+                d.lit = (uint32_t)s->lits.size();
+                d.lit_len = (uint32_t)n.literal.size();
+                s->lits.insert(s->lits.end(), n.literal.begin(), n.literal.end());
+            }
+        }
+    }
+
+    void build_info() {
+        s->col_info.clear();
+        for (size_t c = 0; c < s->col_node.size(); c++) {
+            const Node& n = s->nodes[s->col_node[c]];
+            packos_column_info ci{};
+            switch (n.kind) {
+                case K_INT: ci.kind = PACKOS_KIND_INT; break;
+                case K_UINT: ci.kind = PACKOS_KIND_UINT; break;
+                case K_FLOAT: ci.kind = PACKOS_KIND_FLOAT; break;
+                case K_BOOL: ci.kind = PACKOS_KIND_BOOL; break;
+                case K_STRING: ci.kind = PACKOS_KIND_STRING; break;
+                case K_BYTES: ci.kind = PACKOS_KIND_BYTES; break;
+                case K_TUPLE: ci.kind = PACKOS_KIND_TUPLE; break;
+                case K_MAP: ci.kind = PACKOS_KIND_MAP; break;
+            }
+            bool scalar = n.kind >= K_INT && n.kind <= K_BOOL;
+            ci.width = scalar ? n.width : ((n.kind == K_STRING || n.kind == K_BYTES) && n.width > 0 ? n.width : 0);
+            ci.nullable = scalar ? n.nullable : (n.kind == K_MAP ? 1 : (n.kind == K_TUPLE ? n.nullable : 0));
+            ci.tag = tag_of(n.kind);
+            ci.top_index = n.top;
+            ci.depth = n.depth - 1;
+            snprintf(ci.name, sizeof(ci.name), "%s", n.name.c_str());
+            s->col_info.push_back(ci);
+        }
+    }
+
+    void build_describe() {
+        std::ostringstream o;
+        o << "mode=" << s->mode << " cols=" << s->col_node.size() << " items=" << s->items.size()
+          << " hdrs=" << s->hdrs.size() << " conts=" << s->conts.size() << " var=" << s->has_var
+          << " nullable=" << s->has_nullable << " B=" << s->all_present_size << " fix=" << s->fix_ok
+          << " T=" << s->fix_T << " lds=" << s->fix_lds << " segs=" << s->fsegs.size() << "\n";
+        const char* tn[] = {"HDR", "FIXED", "VAR", "CONST"};
+        for (size_t i = 0; i < s->items.size(); i++) {
+            const EncItem& it = s->items[i];
+            o << "item " << i << " " << tn[it.type] << " cont=" << it.cont << " col=" << it.col
+              << " size=" << it.size << (it.nullable ? " nullable" : "") << (it.is_bool ? " bool" : "") << "\n";
+        }
+        for (const EncHdr& h : s->hdrs)
+            o << "hdr cont=" << h.cont << " j=" << h.j << " tag=" << (int)h.tag
+              << (h.relative ? " rel target=" : " const=") << (h.relative ? h.target : h.value) << "\n";
+        s->describe = o.str();
+    }
+};
+
+}  // namespace
+
+namespace packos {
+void set_error(const std::string& m) { g_err = m; }
+}  // namespace packos
+
+extern "C" {
+
+const char* packos_last_error(void) { return g_err.c_str(); }
+int packos_abi_version(void) { return PACKOS_ABI_VERSION; }
+
+const char* packos_strerror(int code) {
+    switch (code) {
+        case PACKOS_OK: return "ok";
+        case PACKOS_E_INVALID: return "invalid argument";
+        case PACKOS_E_SCHEMA: return "schema rejected";
+        case PACKOS_E_UNSUPPORTED: return "schema feature outside the compiled subset";
+        case PACKOS_E_ALIGN: return "fixed-width column or output not 16-byte aligned";
+        case PACKOS_E_WORKSPACE: return "workspace too small";
+        case PACKOS_E_CAPACITY: return "output arena too small";
+        case PACKOS_E_HIP: return "HIP runtime error";
+        case PACKOS_E_NODEVICE: return "no GPU visible";
+    }
+    return "unknown error";
+}
+
+int packos_schema_compile(const char* schema_json, int mode, packos_schema** out) {
+    if (!schema_json || !out || (mode != PACKOS_MODE_PUTACCESS && mode != PACKOS_MODE_PACKABLE)) {
+        g_err = "packos_schema_compile: bad argument";
+        return PACKOS_E_INVALID;
+    }
+    *out = nullptr;
+    auto* s = new packos_schema();
+    s->mode = mode;
+    try {
+        std::string txt(schema_json);
+        JVal j = JParser(txt).parse();
+        Builder b{s};
+        int root = b.new_node();
+        s->nodes[root].kind = K_ROOT;
+        const JVal* list = nullptr;
+        const JVal* names = nullptr;
+        JVal single;
+        if (j.kind == JVal::ARR) {
+            list = &j;
+        } else if (j.kind == JVal::OBJ && Builder::str_field(j, "type") == "chain") {
+            list = j.get("schema");
+            names = j.get("fieldNames");
+            if (!list || list->kind != JVal::ARR) fail(PACKOS_E_SCHEMA, "chain needs a schema array");
+        } else if (j.kind == JVal::OBJ) {
+            single.kind = JVal::ARR;
+            single.arr.push_back(j);
+            list = &single;
+        } else {
+            fail(PACKOS_E_SCHEMA, "top level must be an array or an object");
+        }
+        for (size_t t = 0; t < list->arr.size(); t++) {
+            std::string nm;
+            if (names && names->kind == JVal::ARR && t < names->arr.size() && names->arr[t].kind == JVal::STR)
+                nm = names->arr[t].str;
+            int id = b.node(list->arr[t], root, 1, (int)t, nm);
+            s->nodes[root].kids.push_back(id);
+        }
+        s->n_top = (int)list->arr.size();
+        b.assign_columns(root);
+        if ((int)s->col_node.size() > kMaxCols) fail(PACKOS_E_UNSUPPORTED, "more than 64 columns");
+        b.build_encode();
+        b.build_fixed();
+        b.build_decode();
+        b.build_info();
+        b.build_describe();
+    } catch (const CompileError& e) {
+        g_err = e.msg;
+        delete s;
+        return e.code;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        delete s;
+        return PACKOS_E_SCHEMA;
+    }
+    *out = s;
+    return PACKOS_OK;
+}
+
+int packos_schema_num_columns(const packos_schema* s) { return s ? (int)s->col_node.size() : -1; }
+int packos_schema_num_top_fields(const packos_schema* s) { return s ? s->n_top : -1; }
+
+int packos_schema_column_info(const packos_schema* s, int col, packos_column_info* out) {
+    if (!s || !out || col < 0 || col >= (int)s->col_info.size()) return PACKOS_E_INVALID;
+    *out = s->col_info[col];
+    return PACKOS_OK;
+}
+
+int64_t packos_schema_fixed_blob_size(const packos_schema* s) {
+    if (!s || s->has_var) return -1;
+    return s->all_present_size;
+}
+
+size_t packos_schema_describe(const packos_schema* s, char* buf, size_t cap) {
+    if (!s) return 0;
+    size_t need = s->describe.size() + 1;
+    if (buf && cap) {
+        size_t n = std::min(cap - 1, s->describe.size());
+        memcpy(buf, s->describe.data(), n);
+        buf[n] = 0;
+    }
+    return need;
+}
+
+int64_t packos_schema_blob_size_host(const packos_schema* s, const uint32_t* widths, const uint8_t* valid) {
+    if (!s) return -1;
+    size_t nc = s->conts.size();
+    std::vector<char> present(nc, 0);
+    for (size_t c = 0; c < nc; c++) {
+        const EncCont& ct = s->conts[c];
+        bool p = ct.parent < 0 ? true : present[ct.parent] != 0;
+        if (p && ct.valid_col >= 0 && valid) p = valid[ct.valid_col] != 0;
+        present[c] = p;
+    }
+    int64_t tot = 0, slack = 0;
+    for (const EncItem& it : s->items) {
+        if (!present[it.cont]) continue;
+        switch (it.type) {
+            case IT_HDR: case IT_CONST: tot += it.size; break;
+            case IT_FIXED:
+                if (it.nullable && valid && !valid[it.col]) slack += it.size;
+                else tot += it.size;
+                break;
+            case IT_VAR: tot += widths ? widths[it.col] : 0; break;
+        }
+    }
+    if (s->mode == PACKOS_MODE_PACKABLE) tot += slack;
+    return tot;
+}
+
+void packos_schema_free(packos_schema* s);  // defined with the device tables (kernels.hip)
+
+}  // extern "C"

@@ -1,0 +1,891 @@
+// kernels.hip — CDNA4 (gfx950) kernels for bulk PackOS encode/decode and the
+// C ABI entry points that launch them (include/packos.h).
+//
+// Hot path (BASELINE.json north_star): encode of millions of same-schema blobs.
+//   k_encode_fixed  fixed-size schemas: a workgroup stages a tile of T blobs'
+//                   input columns in LDS with 16-B coalesced loads, then every
+//                   lane assembles whole 16-B output chunks (constant header /
+//                   key bytes + funnel-shifted column bytes) and stores them
+//                   with global_store_dwordx4.  Pure byte/integer work, HBM
+//                   bound; no MFMA.
+//   k_encode_sizes  var-size schemas, pass 1: blob sizes (thread per blob)
+//   k_scan_*        exclusive scan of blob sizes -> out_offsets
+//   k_encode_var    var-size schemas, pass 2: one wavefront per blob; item
+//                   sizes -> wavefront prefix scan -> header words -> payload
+//                   staged in an LDS slot -> aligned 16-B stores
+//   k_decode        schema.DecodeBuffer semantics (SeqGetAccess + precheck),
+//                   one thread per blob, exact error/panic reporting
+//   k_get_field     GetAccess random-field gather
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "schema_impl.h"
+
+using namespace packos;
+
+#define HIP_TRY(x)                                                                  \
+    do {                                                                            \
+        hipError_t _e = (x);                                                        \
+        if (_e != hipSuccess) {                                                     \
+            set_error(std::string(#x) + ": " + hipGetErrorString(_e));              \
+            return PACKOS_E_HIP;                                                    \
+        }                                                                           \
+    } while (0)
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+constexpr int kSlot = 8192 + 64;      // LDS staging bytes per wavefront (k_encode_var)
+
+__device__ __forceinline__ uint16_t enc_header(int64_t off, int tag) {
+    return (uint16_t)((((uint64_t)off) << 3) & 0xFFFFu) | (uint16_t)(tag & 7);
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        uint32_t t = __shfl_up(x, d, kWave);
+        if (lane >= d) x += t;
+    }
+    return x;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, kWave);
+    return x;
+}
+
+// =========================================================================
+// fixed-size encode
+// =========================================================================
+__global__ __launch_bounds__(kBlock) void k_encode_fixed(FixProgram P, EncCols cols,
+                                                         uint8_t* __restrict__ out, uint64_t n,
+                                                         uint32_t* __restrict__ status,
+                                                         uint32_t st_val) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int T = P.T;
+    const uint32_t B = (uint32_t)P.B;
+    const uint64_t blob0 = (uint64_t)blockIdx.x * (uint64_t)T;
+    const uint32_t rows = (uint32_t)min((uint64_t)T, n - blob0);
+    const int tid = threadIdx.x;
+
+    // descriptor tables -> LDS (after the tile region)
+    uint32_t* s_index = (uint32_t*)(lds + P.lds_bytes);
+    FixSeg* s_segs = (FixSeg*)(lds + P.lds_bytes + ((B + 1) * 4 + 15) / 16 * 16);
+    const uint32_t nsegs = P.seg_index[B];
+    for (uint32_t k = tid; k <= B; k += kBlock) s_index[k] = P.seg_index[k];
+    for (uint32_t k = tid; k < nsegs; k += kBlock) s_segs[k] = P.segs[k];
+
+    // ---- stage the tile's input rows: 16-B coalesced loads -> LDS
+    const int total = P.total_chunks;
+    for (int k0 = 0; k0 < total; k0 += 4 * kBlock) {
+        uint4 v[4];
+        uint32_t dst[4];
+        bool ok[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            int k = k0 + u * kBlock + tid;
+            ok[u] = false;
+            dst[u] = 0;
+            v[u] = make_uint4(0, 0, 0, 0);
+            if (k < total) {
+                int f = 0;
+                while (f + 1 < P.n_fcols && (int)P.fcols[f + 1].chunk_begin <= k) f++;
+                const FixCol fc = P.fcols[f];
+                const uint32_t byte = (uint32_t)(k - (int)fc.chunk_begin) * 16u;
+                const uint32_t lim = rows * fc.width;
+                const uint8_t* src = cols.data[fc.col] + blob0 * fc.width + byte;
+                dst[u] = fc.lds_off + byte;
+                if (byte + 16 <= lim) {
+                    v[u] = *(const uint4*)src;
+                    ok[u] = true;
+                } else if (byte < lim) {
+                    uint32_t w[4] = {0, 0, 0, 0};
+                    for (uint32_t j = 0; j < lim - byte; j++) w[j >> 2] |= (uint32_t)src[j] << (8 * (j & 3));
+                    v[u] = make_uint4(w[0], w[1], w[2], w[3]);
+                    ok[u] = true;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (ok[u]) *(uint4*)(lds + dst[u]) = v[u];
+    }
+    __syncthreads();
+
+    // ---- assemble 16-B output chunks
+    const uint32_t* l32 = (const uint32_t*)lds;
+    const uint32_t tile_bytes = rows * B;
+    uint8_t* obase = out + blob0 * (uint64_t)B;
+    const uint32_t nchunks = (tile_bytes + 15) / 16;
+    for (uint32_t c = tid; c < nchunks; c += kBlock) {
+        uint32_t w0 = 4 * c;
+        uint32_t per = w0 / B;
+        uint32_t r = w0 - per * B;
+        uint32_t o[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            uint32_t v = 0;
+            const uint32_t s1 = s_index[r + 1];
+            for (uint32_t s = s_index[r]; s < s1; s++) {
+                const FixSeg g = s_segs[s];
+                if (g.stride4 == 0) {
+                    v |= g.cval;
+                } else {
+                    const uint32_t addr = (uint32_t)g.a + per * g.stride4;
+                    const uint32_t lo = l32[addr >> 2], hi = l32[(addr >> 2) + 1];
+                    uint32_t x = __builtin_amdgcn_alignbyte(hi, lo, addr & 3) & g.mask;
+                    if (g.cval & 1u) x = x ? (g.mask & 0x01010101u) : 0u;
+                    v |= x;
+                }
+            }
+            o[i] = v;
+            if (++r == B) { r = 0; per++; }
+        }
+        const uint32_t ob = 16 * c;
+        if (ob + 16 <= tile_bytes) {
+            *(uint4*)(obase + ob) = make_uint4(o[0], o[1], o[2], o[3]);
+        } else {
+            for (uint32_t j = 0; ob + j < tile_bytes; j++) obase[ob + j] = (uint8_t)(o[j >> 2] >> (8 * (j & 3)));
+        }
+    }
+    if (status)
+        for (uint32_t i = tid; i < rows; i += kBlock) status[blob0 + i] = st_val;
+}
+
+__global__ void k_fill_offsets(uint64_t* offs, uint64_t n, uint64_t B) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= n) offs[i] = i * B;
+}
+
+// =========================================================================
+// variable-size encode
+// =========================================================================
+struct BlobCtx {
+    uint64_t present;   // container presence bits
+};
+
+__device__ __forceinline__ uint64_t present_mask(const EncProgram& P, const EncCols& cols, uint64_t i) {
+    uint64_t pm = 0;
+    for (int c = 0; c < P.n_conts; c++) {
+        const EncCont ct = P.conts[c];
+        bool p = ct.parent < 0 ? true : ((pm >> ct.parent) & 1ull);
+        if (p && ct.valid_col >= 0) {
+            const uint8_t* v = cols.valid[ct.valid_col];
+            if (v) p = v[i] != 0;
+        }
+        if (p) pm |= 1ull << c;
+    }
+    return pm;
+}
+
+__device__ __forceinline__ uint32_t item_size(const EncItem& it, const EncCols& cols, uint64_t i,
+                                              uint64_t pm, uint32_t* slack) {
+    if (!((pm >> it.cont) & 1ull)) return 0;
+    switch (it.type) {
+        case IT_HDR: case IT_CONST: return it.size;
+        case IT_FIXED:
+            if (it.nullable) {
+                const uint8_t* v = cols.valid[it.col];
+                if (v && !v[i]) { *slack += it.size; return 0; }
+            }
+            return it.size;
+        case IT_VAR: {
+            const uint32_t* o = cols.off[it.col];
+            return o[i + 1] - o[i];
+        }
+    }
+    return 0;
+}
+
+// pass 1: sizes[i] -> offs[i+1]; offs[0] = 0 (thread per blob)
+__global__ __launch_bounds__(kBlock) void k_encode_sizes(EncProgram P, EncCols cols, uint64_t* offs, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) offs[0] = 0;
+    if (i >= n) return;
+    uint64_t pm = present_mask(P, cols, i);
+    uint32_t slack = 0;
+    uint64_t tot = 0;
+    for (int k = 0; k < P.n_items; k++) tot += item_size(P.items[k], cols, i, pm, &slack);
+    if (P.mode == PACKOS_MODE_PACKABLE) tot += slack;
+    offs[i + 1] = tot;
+}
+
+// ---- exclusive scan support (in place over offs[1..n]) -----------------
+constexpr int kScanPer = 4;
+constexpr int kScanTile = kBlock * kScanPer;
+
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x, int lane) {
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        uint64_t t = __shfl_up(x, d, kWave);
+        if (lane >= d) x += t;
+    }
+    return x;
+}
+
+// block-level inclusive scan of kScanTile elements; returns the tile total
+__device__ uint64_t block_scan_tile(uint64_t* v, uint64_t* s_w) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint64_t loc = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++) { loc += v[k]; v[k] = loc; }
+    uint64_t incl = wave_incl_scan64(loc, lane);
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint64_t wave_off = 0, total = 0;
+    for (int w = 0; w < kWavesPerBlock; w++) {
+        if (w < wave) wave_off += s_w[w];
+        total += s_w[w];
+    }
+    uint64_t excl = wave_off + incl - loc;
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++) v[k] += excl;
+    __syncthreads();
+    return total;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_tiles(uint64_t* x, uint64_t n, uint64_t* sums) {
+    __shared__ uint64_t s_w[kWavesPerBlock];
+    uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+    uint64_t v[kScanPer];
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++) v[k] = base + k < n ? x[base + k] : 0;
+    uint64_t total = block_scan_tile(v, s_w);
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++)
+        if (base + k < n) x[base + k] = v[k];
+    if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+// exclusive scan of the tile sums, one workgroup, any count
+__global__ __launch_bounds__(kBlock) void k_scan_sums(uint64_t* sums, uint64_t nb) {
+    __shared__ uint64_t s_w[kWavesPerBlock];
+    uint64_t carry = 0;
+    for (uint64_t t0 = 0; t0 < nb; t0 += kScanTile) {
+        uint64_t base = t0 + (uint64_t)threadIdx.x * kScanPer;
+        uint64_t v[kScanPer], raw[kScanPer];
+#pragma unroll
+        for (int k = 0; k < kScanPer; k++) { raw[k] = v[k] = base + k < nb ? sums[base + k] : 0; }
+        uint64_t total = block_scan_tile(v, s_w);
+#pragma unroll
+        for (int k = 0; k < kScanPer; k++)
+            if (base + k < nb) sums[base + k] = carry + v[k] - raw[k];
+        carry += total;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_add(uint64_t* x, uint64_t n, const uint64_t* sums) {
+    uint64_t add = sums[blockIdx.x];
+    uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+#pragma unroll
+    for (int k = 0; k < kScanPer; k++)
+        if (base + k < n) x[base + k] += add;
+}
+
+// pass 2: one wavefront per blob
+__global__ __launch_bounds__(kBlock) void k_encode_var(EncProgram P, EncCols cols, const uint64_t* __restrict__ offs,
+                                                       uint64_t stride, uint8_t* __restrict__ out, uint64_t cap,
+                                                       uint64_t n, uint32_t* __restrict__ status) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int npos = P.n_items + 1;
+    const int wave_bytes = kSlot + ((npos * 4 + 15) / 16) * 16;
+    uint8_t* slot = lds + wave * wave_bytes;
+    uint32_t* pos = (uint32_t*)(slot + kSlot);
+
+    for (uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + wave; i < n;
+         i += (uint64_t)gridDim.x * kWavesPerBlock) {
+        const uint64_t pm = present_mask(P, cols, i);
+        // item sizes -> wavefront prefix scan -> positions
+        uint32_t running = 0, slack = 0;
+        for (int b = 0; b < P.n_items; b += kWave) {
+            const int k = b + lane;
+            uint32_t sz = 0;
+            if (k < P.n_items) sz = item_size(P.items[k], cols, i, pm, &slack);
+            const uint32_t incl = wave_incl_scan(sz, lane);
+            if (k < P.n_items) pos[k] = running + incl - sz;
+            running += __shfl(incl, kWave - 1, kWave);
+        }
+        slack = wave_sum(slack);
+        const uint32_t payload_end = running;
+        const uint32_t total = running + (P.mode == PACKOS_MODE_PACKABLE ? slack : 0u);
+        if (lane == 0) pos[P.n_items] = running;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        const uint64_t o = offs ? offs[i] : i * stride;
+        if (o + total > cap) {
+            if (status && lane == 0) status[i] = (uint32_t)PACKOS_ERR_ENCODE;
+            continue;
+        }
+        const bool staged = total + 16 <= (uint32_t)kSlot;
+        uint8_t* dst = staged ? (slot + (o & 15)) : (out + o);
+
+        // header words (lane per header)
+        bool ovf = false;
+        for (int b = 0; b < P.n_hdrs; b += kWave) {
+            const int k = b + lane;
+            if (k < P.n_hdrs) {
+                const EncHdr h = P.hdrs[k];
+                if ((pm >> h.cont) & 1ull) {
+                    const uint32_t hpos = pos[h.hdr_item];
+                    uint16_t v;
+                    if (h.relative) {
+                        const int64_t off = (int64_t)pos[h.target] - (int64_t)(hpos + P.items[h.hdr_item].size);
+                        ovf |= off >= 8192;
+                        v = enc_header(off, h.tag);
+                    } else {
+                        v = h.value;
+                        ovf |= h.ovf != 0;
+                    }
+                    dst[hpos + 2 * h.j] = (uint8_t)v;
+                    dst[hpos + 2 * h.j + 1] = (uint8_t)(v >> 8);
+                }
+            }
+        }
+        // payload bytes (wave per item)
+        for (int k = 0; k < P.n_items; k++) {
+            const EncItem it = P.items[k];
+            if (it.type == IT_HDR) continue;
+            const uint32_t p0 = pos[k], p1 = pos[k + 1];
+            const uint32_t len = p1 - p0;
+            if (len == 0) continue;
+            const uint8_t* src;
+            if (it.type == IT_CONST) src = P.lits + it.lit;
+            else if (it.type == IT_FIXED) src = cols.data[it.col] + i * (uint64_t)it.size;
+            else src = cols.data[it.col] + cols.off[it.col][i];
+            if (it.is_bool) {
+                if (lane == 0) dst[p0] = src[0] != 0;
+            } else {
+                for (uint32_t j = lane; j < len; j += kWave) dst[p0 + j] = src[j];
+            }
+        }
+        // packable.Pack slack: zero bytes after the End-marked payload
+        for (uint32_t j = lane; j < total - payload_end; j += kWave) dst[payload_end + j] = 0;
+        if (staged) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t mis = (uint32_t)(o & 15);
+            const uint32_t head = min(total, (16u - mis) & 15u);
+            if ((uint32_t)lane < head) out[o + lane] = dst[lane];
+            const uint32_t body = (total - head) / 16;
+            const uint8_t* sb = dst + head;              // 16-B aligned in LDS
+            uint8_t* gb = out + o + head;                // 16-B aligned in HBM
+            for (uint32_t c = lane; c < body; c += kWave) *(uint4*)(gb + 16 * c) = *(const uint4*)(sb + 16 * c);
+            const uint32_t done = head + body * 16;
+            if ((uint32_t)lane < total - done) out[o + done + lane] = dst[done + lane];
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (status && lane == 0) status[i] = ovf ? PACKOS_STATUS_OVERFLOW13 : 0u;
+        // make sure no lane reuses the slot before every lane has read it
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// =========================================================================
+// decode: schema.DecodeBuffer, one thread per blob
+// =========================================================================
+constexpr int kDecDepth = 8;
+
+struct DSeq {
+    int64_t len, base, count, pos, next_off, cur_off;
+    uint64_t start;     // absolute arena offset of this (sub)buffer
+    int next_type, cur_type;
+};
+
+__device__ __forceinline__ uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+
+// NewSeqGetAccess (seqget.go:22-47)
+__device__ __forceinline__ int dseq_init(DSeq& s, const uint8_t* a, uint64_t start, int64_t len) {
+    if (len < 4) return 1;
+    const uint16_t h0 = rd16(a + start);
+    const int64_t base = h0 >> 3;
+    if (len < base) return 1;
+    const uint16_t h1 = rd16(a + start + 2);
+    s.len = len; s.base = base; s.count = base / 2; s.pos = 0; s.start = start;
+    s.cur_off = base; s.cur_type = h0 & 7;
+    s.next_off = (h1 >> 3) + base; s.next_type = h1 & 7;
+    return 0;
+}
+// Advance (seqget.go:85-103): 0 ok, 1 out of bounds, 2 Go panic (unchecked header read)
+__device__ __forceinline__ int dseq_advance(DSeq& s, const uint8_t* a) {
+    if (s.pos + 2 > s.count) return 1;
+    s.pos++;
+    s.cur_off = s.next_off;
+    s.cur_type = s.next_type;
+    if (s.cur_type != 0) {
+        if ((s.pos + 1) * 2 + 2 > s.len) return 2;
+        const uint16_t h = rd16(a + s.start + (s.pos + 1) * 2);
+        s.next_off = (h >> 3) + s.base;
+        s.next_type = h & 7;
+    }
+    return 0;
+}
+// precheck (schema.go:997-1013): 0 ok else ErrConstraintViolated
+__device__ __forceinline__ int dprecheck(const DSeq& s, int tag, int64_t hint, bool nullable, int64_t& w) {
+    if (s.pos >= s.count) return 3;
+    if (s.next_off > s.len) return 3;
+    if (s.cur_type != tag) return 3;
+    w = s.next_off - s.cur_off;
+    if (!nullable && hint != 0 && w != hint) return 3;
+    return 0;
+}
+
+constexpr int kPanic = 0x100;
+
+struct Frame {
+    DSeq q;
+    int node;
+    int k;
+};
+
+__global__ __launch_bounds__(kBlock) void k_decode(DecProgram P, DecCols cols, const uint8_t* __restrict__ arena,
+                                                   const uint64_t* __restrict__ offs, uint64_t stride, uint64_t n,
+                                                   uint32_t* __restrict__ status) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t a0 = offs ? offs[i] : i * stride;
+    const uint64_t a1 = offs ? offs[i + 1] : (i + 1) * stride;
+    Frame st[kDecDepth];
+    int d = 0;
+    if (dseq_init(st[0].q, arena, a0, (int64_t)(a1 - a0))) {
+        status[i] = (uint32_t)PACKOS_ERR_INVALID_FORMAT;  // position -1
+        return;
+    }
+    st[0].node = P.root;
+    st[0].k = 0;
+    int err = 0;
+    for (;;) {
+        Frame& f = st[d];
+        const DecNode fn = P.nodes[f.node];
+        if (f.k >= fn.nkids) {
+            if (d == 0) break;
+            d--;  // container finished: Advance the parent past it
+            const int a = dseq_advance(st[d].q, arena);
+            if (a) { err = a == 2 ? kPanic : 2; break; }
+            st[d].k++;
+            continue;
+        }
+        const int nid = P.kids[fn.kid0 + f.k];
+        const DecNode nd = P.nodes[nid];
+        DSeq& q = f.q;
+        int64_t w = 0;
+        if (nd.kind == K_TUPLE || nd.kind == K_MAP) {
+            err = dprecheck(q, nd.tag, -1, nd.nullable, w);
+            if (err) break;
+            if (nd.kind == K_MAP && (nd.nkids & 1)) { err = 3; break; }
+            if (cols.valid[nd.col]) cols.valid[nd.col][i] = w != 0;
+            if (w != 0) {
+                // PeekNestedSeq (seqget.go:105-121)
+                if (q.next_off - q.cur_off <= 0 || q.next_off > q.len) { err = 1; break; }
+                if (d + 1 >= kDecDepth) { err = 1; break; }
+                Frame& c = st[d + 1];
+                if (dseq_init(c.q, arena, q.start + q.cur_off, q.next_off - q.cur_off)) { err = 1; break; }
+                if (nd.kind == K_TUPLE && nd.nkids > 0 && (c.q.count - 1) != nd.nkids && !nd.variable) {
+                    err = 3;
+                    break;
+                }
+                c.node = nid;
+                c.k = 0;
+                d++;
+                continue;
+            }
+            const int a = dseq_advance(q, arena);
+            if (a) { err = a == 2 ? kPanic : 2; break; }
+            f.k++;
+            continue;
+        }
+        // primitives: validatePrimitiveAndGetPayload (schema.go:1031-1052)
+        const int64_t hint = nd.width;
+        err = dprecheck(q, nd.tag, hint, nd.nullable, w);
+        if (err) break;
+        const int64_t ps = w > 0 ? q.cur_off : -1;
+        {
+            const int a = dseq_advance(q, arena);
+            if (a) { err = a == 2 ? kPanic : 2; break; }
+        }
+        const uint8_t* pay = arena + q.start + (ps < 0 ? 0 : ps);
+        switch (nd.kind) {
+            case K_INT: case K_UINT: case K_FLOAT: case K_BOOL: {
+                if (ps < 0) {
+                    if (cols.valid[nd.col]) cols.valid[nd.col][i] = 0;
+                    break;
+                }
+                if (w < nd.width) { err = kPanic; break; }  // LittleEndian.UintXX on a short slice
+                uint8_t* dstp = cols.data[nd.col] + i * (uint64_t)nd.width;
+                if (nd.kind == K_BOOL) dstp[0] = pay[0] != 0;
+                else for (int j = 0; j < nd.width; j++) dstp[j] = pay[j];
+                if (cols.valid[nd.col]) cols.valid[nd.col][i] = 1;
+                break;
+            }
+            case K_STRING: case K_BYTES:
+                if (nd.width > 0) {
+                    uint8_t* dstp = cols.data[nd.col] + i * (uint64_t)nd.width;
+                    for (int j = 0; j < nd.width; j++) dstp[j] = pay[j];
+                } else {
+                    cols.start[nd.col][i] = ps < 0 ? 0ull : q.start + (uint64_t)ps;
+                    cols.length[nd.col][i] = ps < 0 ? 0u : (uint32_t)w;
+                }
+                break;
+            case K_MATCH: {
+                const uint32_t have = ps < 0 ? 0u : (uint32_t)w;
+                bool eq = have == nd.lit_len;
+                for (uint32_t j = 0; eq && j < have; j++) eq = pay[j] == P.lits[nd.lit + j];
+                if (!eq) err = PACKOS_ERR_STRING_MATCH;
+                break;
+            }
+        }
+        if (err) break;
+        f.k++;
+    }
+    uint32_t sv = 0;
+    if (err) {
+        const uint32_t posv = (uint32_t)(st[0].k + 1) << 8;
+        if (err == kPanic) sv = PACKOS_STATUS_PANIC | posv;
+        else sv = (uint32_t)(d == 0 ? err : PACKOS_ERR_INVALID_FORMAT) | posv;
+    }
+    status[i] = sv;
+}
+
+// =========================================================================
+// GetAccess gather
+// =========================================================================
+struct DGet {
+    uint64_t start;
+    int64_t len, base, argc;
+};
+__device__ __forceinline__ bool dget_init(DGet& g, const uint8_t* a, uint64_t start, int64_t len) {
+    if (len < 2) return false;
+    g.base = rd16(a + start) >> 3;
+    if (len < g.base) return false;
+    g.start = start; g.len = len; g.argc = g.base / 2 - 1;
+    return true;
+}
+// rangeAt (get.go:38-58)
+__device__ __forceinline__ void dget_range(const DGet& g, const uint8_t* a, int64_t pos, int& tp, int64_t& s,
+                                           int64_t& e) {
+    if (pos >= g.argc) { tp = 0; s = -2; e = -1; return; }
+    const uint16_t h1 = rd16(a + g.start + pos * 2), h2 = rd16(a + g.start + (pos + 1) * 2);
+    s = h1 >> 3; tp = h1 & 7;
+    e = (h2 >> 3) + g.base;
+    if (pos > 0) s += g.base;
+    if (e > g.len) e = -1;
+}
+
+struct PathArg {
+    int32_t p[16];
+};
+
+__global__ __launch_bounds__(kBlock) void k_get_field(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
+                                                      uint64_t stride, uint64_t n, PathArg path, int depth, int want_tag, int want_width, uint64_t* out_start,
+                                                      uint32_t* out_len, uint8_t* out_tag, uint8_t* status) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t a0 = offs ? offs[i] : i * stride;
+    const uint64_t a1 = offs ? offs[i + 1] : (i + 1) * stride;
+    out_start[i] = 0; out_len[i] = 0; out_tag[i] = 0;
+    DGet g;
+    if (!dget_init(g, arena, a0, (int64_t)(a1 - a0))) { status[i] = 3; return; }
+    int tp; int64_t s, e;
+    for (int d = 0; d < depth - 1; d++) {
+        dget_range(g, arena, path.p[d], tp, s, e);
+        if (e < s || (tp != 7 && tp != 4)) { status[i] = 1; return; }
+        if (e == s) { status[i] = 2; return; }
+        DGet nx;
+        if (!dget_init(nx, arena, g.start + (uint64_t)s, e - s)) { status[i] = 3; return; }
+        g = nx;
+    }
+    dget_range(g, arena, path.p[depth - 1], tp, s, e);
+    out_tag[i] = (uint8_t)tp;
+    const bool ok = want_width >= 0 ? (tp == want_tag && e - s == want_width) : (tp == want_tag && e >= s);
+    if (!ok) { status[i] = 1; return; }
+    out_start[i] = g.start + (uint64_t)s;
+    out_len[i] = (uint32_t)(e - s);
+    status[i] = 0;
+}
+
+// =========================================================================
+// host helpers
+// =========================================================================
+template <typename T>
+size_t put_bytes(std::vector<uint8_t>& blob, const std::vector<T>& v) {
+    size_t off = (blob.size() + 15) / 16 * 16;
+    blob.resize(off + v.size() * sizeof(T) + 16);
+    if (!v.empty()) memcpy(blob.data() + off, v.data(), v.size() * sizeof(T));
+    return off;
+}
+
+int current_device(int* dev) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+        set_error("no GPU visible");
+        return PACKOS_E_NODEVICE;
+    }
+    HIP_TRY(hipGetDevice(dev));
+    return PACKOS_OK;
+}
+
+int fill_enc_cols(const packos_schema* s, const packos_column* cols, EncCols& ec, bool* any_nil) {
+    memset(&ec, 0, sizeof(ec));
+    *any_nil = false;
+    for (size_t c = 0; c < s->col_node.size(); c++) {
+        const Node& n = s->nodes[s->col_node[c]];
+        ec.data[c] = (const uint8_t*)cols[c].data;
+        ec.off[c] = cols[c].offsets;
+        ec.valid[c] = cols[c].valid;
+        bool scalar = n.kind >= K_INT && n.kind <= K_BOOL;
+        bool fixed_str = (n.kind == K_STRING || n.kind == K_BYTES) && n.width > 0;
+        bool var = (n.kind == K_STRING || n.kind == K_BYTES) && n.width <= 0;
+        if ((scalar || fixed_str || var) && !ec.data[c]) {
+            set_error("column " + std::to_string(c) + " has no data pointer");
+            return PACKOS_E_INVALID;
+        }
+        if (var && !ec.off[c]) {
+            set_error("var-width column " + std::to_string(c) + " has no offsets");
+            return PACKOS_E_INVALID;
+        }
+        if (!(scalar && n.nullable) && !(n.kind == K_TUPLE && n.nullable) && n.kind != K_MAP) ec.valid[c] = nullptr;
+        if (ec.valid[c]) *any_nil = true;
+    }
+    return PACKOS_OK;
+}
+
+}  // namespace
+
+// =========================================================================
+// per-device program tables
+// =========================================================================
+int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
+    std::lock_guard<std::mutex> lk(s->mu);
+    for (auto& d : s->dev)
+        if (d.device == device) { *out = &d; return PACKOS_OK; }
+    std::vector<uint8_t> blob;
+    size_t o_items = put_bytes(blob, s->items);
+    size_t o_hdrs = put_bytes(blob, s->hdrs);
+    size_t o_conts = put_bytes(blob, s->conts);
+    size_t o_lits = put_bytes(blob, s->lits);
+    size_t o_fsegs = put_bytes(blob, s->fsegs);
+    size_t o_fidx = put_bytes(blob, s->fseg_index);
+    size_t o_fcols = put_bytes(blob, s->fcols);
+    size_t o_dnodes = put_bytes(blob, s->dnodes);
+    size_t o_dkids = put_bytes(blob, s->dkids);
+    DeviceTables t;
+    t.device = device;
+    HIP_TRY(hipMalloc(&t.block, blob.size()));
+    HIP_TRY(hipMemcpy(t.block, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    uint8_t* b = (uint8_t*)t.block;
+    t.enc.items = (const EncItem*)(b + o_items);
+    t.enc.hdrs = (const EncHdr*)(b + o_hdrs);
+    t.enc.conts = (const EncCont*)(b + o_conts);
+    t.enc.lits = b + o_lits;
+    t.enc.n_items = (int)s->items.size();
+    t.enc.n_hdrs = (int)s->hdrs.size();
+    t.enc.n_conts = (int)s->conts.size();
+    t.enc.mode = s->mode;
+    t.fix.segs = (const FixSeg*)(b + o_fsegs);
+    t.fix.seg_index = (const uint32_t*)(b + o_fidx);
+    t.fix.fcols = (const FixCol*)(b + o_fcols);
+    t.fix.B = (int)s->all_present_size;
+    t.fix.T = s->fix_T;
+    t.fix.n_fcols = (int)s->fcols.size();
+    t.fix.lds_bytes = s->fix_lds;
+    t.fix.total_chunks = s->fix_chunks;
+    t.fix.overflow = s->all_present_overflow;
+    t.dec.nodes = (const DecNode*)(b + o_dnodes);
+    t.dec.kids = (const int32_t*)(b + o_dkids);
+    t.dec.lits = b + o_lits;
+    t.dec.root = 0;
+    s->dev.push_back(t);
+    *out = &s->dev.back();
+    return PACKOS_OK;
+}
+
+extern "C" {
+
+void packos_schema_free(packos_schema* s) {
+    if (!s) return;
+    for (auto& d : s->dev) {
+        if (d.block) {
+            int cur = -1;
+            (void)hipGetDevice(&cur);
+            (void)hipSetDevice(d.device);
+            (void)hipFree(d.block);
+            if (cur >= 0) (void)hipSetDevice(cur);
+        }
+    }
+    delete s;
+}
+
+size_t packos_encode_workspace_size(const packos_schema* s, size_t n_blobs) {
+    (void)s;
+    size_t nb = (n_blobs + kScanTile - 1) / kScanTile;
+    return (nb + 16) * sizeof(uint64_t);
+}
+
+static int size_pass(packos_schema* s, DeviceTables* t, const EncCols& ec, size_t n, uint64_t* offs, void* ws,
+                     size_t ws_bytes, hipStream_t st) {
+    if (!offs) { set_error("out_offsets required for a variable-size schema"); return PACKOS_E_INVALID; }
+    size_t nb = (n + kScanTile - 1) / kScanTile;
+    if (!ws || ws_bytes < packos_encode_workspace_size(s, n)) {
+        set_error("workspace too small");
+        return PACKOS_E_WORKSPACE;
+    }
+    const unsigned g = (unsigned)((n + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_encode_sizes, dim3(std::max(1u, g)), dim3(kBlock), 0, st, t->enc, ec, offs, (uint64_t)n);
+    if (n) {
+        uint64_t* sums = (uint64_t*)ws;
+        hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)nb), dim3(kBlock), 0, st, offs + 1, (uint64_t)n, sums);
+        hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kBlock), 0, st, sums, (uint64_t)nb);
+        hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(kBlock), 0, st, offs + 1, (uint64_t)n,
+                           (const uint64_t*)sums);
+    }
+    HIP_TRY(hipGetLastError());
+    return PACKOS_OK;
+}
+
+int packos_encoded_size_batch(const packos_schema* cs, const packos_column* cols, size_t n, uint64_t* out_offsets,
+                              void* ws, size_t ws_bytes, void* stream) {
+    packos_schema* s = const_cast<packos_schema*>(cs);
+    if (!s || !cols || !out_offsets) return PACKOS_E_INVALID;
+    int dev, r;
+    if ((r = current_device(&dev))) return r;
+    DeviceTables* t;
+    if ((r = upload_tables(s, dev, &t))) return r;
+    EncCols ec;
+    bool any_nil;
+    if ((r = fill_enc_cols(s, cols, ec, &any_nil))) return r;
+    hipStream_t st = (hipStream_t)stream;
+    if (!s->has_var && !any_nil) {
+        hipLaunchKernelGGL(k_fill_offsets, dim3((unsigned)((n + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                           out_offsets, (uint64_t)n, (uint64_t)s->all_present_size);
+        HIP_TRY(hipGetLastError());
+        return PACKOS_OK;
+    }
+    return size_pass(s, t, ec, n, out_offsets, ws, ws_bytes, st);
+}
+
+int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size_t n, uint8_t* out, uint64_t cap,
+                        uint64_t* out_offsets, uint32_t* status, void* ws, size_t ws_bytes, uint32_t flags,
+                        void* stream) {
+    packos_schema* s = const_cast<packos_schema*>(cs);
+    if (!s || !cols || (!out && n)) { set_error("packos_encode_batch: bad argument"); return PACKOS_E_INVALID; }
+    if (n == 0) return PACKOS_OK;
+    int dev, r;
+    if ((r = current_device(&dev))) return r;
+    DeviceTables* t;
+    if ((r = upload_tables(s, dev, &t))) return r;
+    EncCols ec;
+    bool any_nil;
+    if ((r = fill_enc_cols(s, cols, ec, &any_nil))) return r;
+    hipStream_t st = (hipStream_t)stream;
+    const bool fixed_size = !s->has_var && !any_nil;
+    if (fixed_size) {
+        const uint64_t B = (uint64_t)s->all_present_size;
+        if (B * n > cap) { set_error("output arena too small"); return PACKOS_E_CAPACITY; }
+        if (out_offsets) {
+            hipLaunchKernelGGL(k_fill_offsets, dim3((unsigned)((n + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                               st, out_offsets, (uint64_t)n, B);
+        }
+        bool aligned = ((uintptr_t)out & 15) == 0;
+        for (const FixCol& fc : s->fcols) aligned = aligned && (((uintptr_t)ec.data[fc.col]) & 15) == 0;
+        if (s->fix_ok && B >= 4 && aligned) {
+            const uint64_t tiles = (n + s->fix_T - 1) / s->fix_T;
+            const size_t lds = (size_t)s->fix_lds + ((B + 1) * 4 + 15) / 16 * 16 + s->fsegs.size() * sizeof(FixSeg);
+            const uint32_t stv = s->all_present_overflow ? PACKOS_STATUS_OVERFLOW13 : 0u;
+            hipLaunchKernelGGL(k_encode_fixed, dim3((unsigned)tiles), dim3(kBlock), lds, st, t->fix, ec, out,
+                               (uint64_t)n, status, stv);
+            HIP_TRY(hipGetLastError());
+            return PACKOS_OK;
+        }
+        // large or unaligned fixed blobs: general kernel with a stride
+        const size_t npos = s->items.size() + 1;
+        const size_t lds = (size_t)kWavesPerBlock * (kSlot + ((npos * 4 + 15) / 16) * 16);
+        const unsigned grid = (unsigned)std::min<uint64_t>((n + kWavesPerBlock - 1) / kWavesPerBlock, 256 * 16);
+        hipLaunchKernelGGL(k_encode_var, dim3(grid), dim3(kBlock), lds, st, t->enc, ec, (const uint64_t*)nullptr, B,
+                           out, cap, (uint64_t)n, status);
+        HIP_TRY(hipGetLastError());
+        return PACKOS_OK;
+    }
+    if (!(flags & PACKOS_ENC_OFFSETS_READY)) {
+        if ((r = size_pass(s, t, ec, n, out_offsets, ws, ws_bytes, st))) return r;
+    } else if (!out_offsets) {
+        set_error("PACKOS_ENC_OFFSETS_READY without out_offsets");
+        return PACKOS_E_INVALID;
+    }
+    const size_t npos = s->items.size() + 1;
+    const size_t lds = (size_t)kWavesPerBlock * (kSlot + ((npos * 4 + 15) / 16) * 16);
+    if (lds > 64 * 1024) { set_error("schema has too many items for the LDS budget"); return PACKOS_E_UNSUPPORTED; }
+    const unsigned grid = (unsigned)std::min<uint64_t>((n + kWavesPerBlock - 1) / kWavesPerBlock, 256 * 16);
+    hipLaunchKernelGGL(k_encode_var, dim3(grid), dim3(kBlock), lds, st, t->enc, ec, (const uint64_t*)out_offsets,
+                       (uint64_t)0, out, cap, (uint64_t)n, status);
+    HIP_TRY(hipGetLastError());
+    return PACKOS_OK;
+}
+
+int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
+                        size_t n, packos_column* out_cols, uint32_t* status, void* stream) {
+    packos_schema* s = const_cast<packos_schema*>(cs);
+    if (!s || !out_cols || !status || (!arena && n)) { set_error("packos_decode_batch: bad argument"); return PACKOS_E_INVALID; }
+    if (n == 0) return PACKOS_OK;
+    if (!offsets && stride == 0) { set_error("offsets or stride required"); return PACKOS_E_INVALID; }
+    int dev, r;
+    if ((r = current_device(&dev))) return r;
+    DeviceTables* t;
+    if ((r = upload_tables(s, dev, &t))) return r;
+    int maxd = 0;
+    for (const Node& nd : s->nodes) maxd = std::max(maxd, nd.depth);
+    if (maxd >= kDecDepth) { set_error("schema nesting too deep for the decoder"); return PACKOS_E_UNSUPPORTED; }
+    DecCols dc;
+    memset(&dc, 0, sizeof(dc));
+    for (size_t c = 0; c < s->col_node.size(); c++) {
+        const Node& nd = s->nodes[s->col_node[c]];
+        dc.data[c] = (uint8_t*)out_cols[c].data;
+        dc.valid[c] = out_cols[c].valid;
+        dc.start[c] = out_cols[c].start;
+        dc.length[c] = out_cols[c].length;
+        bool scalar = nd.kind >= K_INT && nd.kind <= K_BOOL;
+        bool fixed_str = (nd.kind == K_STRING || nd.kind == K_BYTES) && nd.width > 0;
+        bool var = (nd.kind == K_STRING || nd.kind == K_BYTES) && nd.width <= 0;
+        if ((scalar || fixed_str) && !dc.data[c]) { set_error("decode column " + std::to_string(c) + " needs data"); return PACKOS_E_INVALID; }
+        if (var && (!dc.start[c] || !dc.length[c])) { set_error("decode var column " + std::to_string(c) + " needs start/length"); return PACKOS_E_INVALID; }
+        if (scalar && nd.nullable && !dc.valid[c]) { set_error("decode nullable column " + std::to_string(c) + " needs valid"); return PACKOS_E_INVALID; }
+        if (!(scalar && nd.nullable) && nd.kind != K_TUPLE && nd.kind != K_MAP) dc.valid[c] = nullptr;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_decode, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, t->dec, dc, arena,
+                       offsets, stride, (uint64_t)n, status);
+    HIP_TRY(hipGetLastError());
+    return PACKOS_OK;
+}
+
+int packos_get_field_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride, size_t n,
+                           const int32_t* path, int depth, int want_tag, int want_width, uint64_t* out_start,
+                           uint32_t* out_len, uint8_t* out_tag, uint8_t* status, void* stream) {
+    if (!path || depth < 1 || depth > 16 || !out_start || !out_len || !out_tag || !status || (!arena && n))
+        return PACKOS_E_INVALID;
+    if (n == 0) return PACKOS_OK;
+    if (!offsets && stride == 0) return PACKOS_E_INVALID;
+    int dev, r;
+    if ((r = current_device(&dev))) return r;
+    PathArg pa{};
+    for (int d = 0; d < depth; d++) {
+        if (path[d] < 0) { set_error("negative field position"); return PACKOS_E_INVALID; }
+        pa.p[d] = path[d];
+    }
+    hipLaunchKernelGGL(k_get_field, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)stream, arena, offsets, stride, (uint64_t)n, pa, depth, want_tag, want_width,
+                       out_start, out_len, out_tag, status);
+    HIP_TRY(hipGetLastError());
+    return PACKOS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,123 @@
+// program.h — compiled schema programs shared by the host compiler
+// (compile.cpp) and the HIP kernels (kernels.hip).  Plain POD structs.
+#pragma once
+#include <stdint.h>
+
+namespace packos {
+
+constexpr int kMaxCols = 64;      // columns per schema (kernel-argument tables)
+constexpr int kMaxDepth = 16;     // nesting depth supported by the decoders
+constexpr int kMaxConts = 64;     // containers per schema (bitmask in the encoder)
+
+enum NodeKind : int32_t {
+    K_INT = 1, K_UINT = 2, K_FLOAT = 3, K_BOOL = 4, K_STRING = 5, K_BYTES = 6,
+    K_MATCH = 7, K_TUPLE = 8, K_MAP = 9, K_ROOT = 10
+};
+
+// ---------------------------------------------------------------- encode ----
+// Items are the byte runs of one blob in wire order.  Positions are the
+// exclusive prefix sum of item sizes; header words are differences of
+// positions (the h0 / End / relative-offset rules of access/put.go:619-652
+// and packable/pack.go:30-57).
+enum : uint8_t { IT_HDR = 0, IT_FIXED = 1, IT_VAR = 2, IT_CONST = 3 };
+
+struct EncItem {
+    uint8_t type;      // IT_*
+    uint8_t nullable;  // fixed leaf with a validity column
+    uint8_t is_bool;   // normalise any non-zero input byte to 1
+    uint8_t pad;
+    int16_t cont;      // container whose presence gates this item
+    int16_t col;       // leaf column (IT_FIXED / IT_VAR), -1 otherwise
+    uint32_t size;     // fixed width / literal length / header-block bytes
+    uint32_t lit;      // literal offset (IT_CONST)
+};
+
+struct EncHdr {            // one uint16 header word
+    uint16_t hdr_item;     // the container's IT_HDR item
+    uint16_t target;       // item whose position the offset points to
+    uint16_t cont;         // container id (gates the write)
+    uint8_t tag;
+    uint8_t relative;      // 0 = constant `value`, 1 = pos(target) - payload start
+    uint16_t j;            // index within the header block
+    uint16_t value;        // constant word (h0, or 0x0010 for an empty nested block)
+    uint16_t ovf;          // constant word overflowed 13 bits
+    uint16_t pad;
+};
+
+struct EncCont {
+    int16_t parent;        // -1 for the root (the chain itself)
+    int16_t valid_col;     // column holding the nil flag, -1 if never nil
+    uint16_t hdr_item;
+    uint16_t n_kids;
+};
+
+struct EncProgram {
+    const EncItem* items;
+    const EncHdr* hdrs;
+    const EncCont* conts;
+    const uint8_t* lits;
+    int32_t n_items, n_hdrs, n_conts, mode;
+};
+
+// Fixed-size layout (no var-width leaves, no nils in the call): every blob is
+// B bytes and byte q of a blob is either a constant or byte `off` of a fixed
+// column row.  The kernel works on tiles of T blobs; for each dword r of a
+// 4-blob period (4B bytes = B dwords) a short list of segments says where its
+// bytes come from in the LDS-staged input tile.
+struct FixSeg {
+    int32_t a;          // LDS byte address of dword byte 0 for the period's blob 0
+    uint32_t stride4;   // LDS bytes between periods (4 * column width); 0 = constant
+    uint32_t mask;      // byte-lane mask of this segment within the dword
+    uint32_t cval;      // constant bytes (stride4 == 0) or flags (bit0: bool normalise)
+};
+
+struct FixCol {
+    int32_t col;         // column index
+    uint32_t width;      // row width in bytes
+    uint32_t lds_off;    // LDS offset of this column's tile region
+    uint32_t chunk_begin;// first 16-byte chunk of this column within the tile
+};
+
+struct FixProgram {
+    const FixSeg* segs;
+    const uint32_t* seg_index;   // B+1 entries: segments of period-dword r
+    const FixCol* fcols;
+    int32_t B, T, n_fcols, lds_bytes, total_chunks, overflow;
+};
+
+// ---------------------------------------------------------------- decode ----
+struct DecNode {
+    int32_t kind;      // NodeKind
+    int32_t width;     // scalar width, or SchemaString/SchemaBytes Width
+    int32_t col;       // column, -1 for K_MATCH / K_ROOT
+    int32_t nkids;
+    int32_t kid0;      // first entry in the kid list
+    uint8_t nullable;  // precheck nullable flag (schema IsNullable())
+    uint8_t variable;  // TupleSchema.VariableLength
+    uint8_t tag;
+    uint8_t pad;
+    uint32_t lit, lit_len;
+};
+
+struct DecProgram {
+    const DecNode* nodes;
+    const int32_t* kids;
+    const uint8_t* lits;
+    int32_t root;
+};
+
+// column pointer tables passed by value as kernel arguments
+struct EncCols {
+    const uint8_t* data[kMaxCols];
+    const uint32_t* off[kMaxCols];
+    const uint8_t* valid[kMaxCols];
+};
+
+struct DecCols {
+    uint8_t* data[kMaxCols];
+    uint8_t* valid[kMaxCols];
+    uint64_t* start[kMaxCols];
+    uint32_t* length[kMaxCols];
+};
+
+}  // namespace packos

@@ -1,0 +1,75 @@
+// schema_impl.h — host representation of a compiled schema (packos_schema).
+#pragma once
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/packos.h"
+#include "program.h"
+
+namespace packos {
+
+struct Node {
+    int kind = 0;          // NodeKind
+    int width = 0;         // scalar width / SchemaString|SchemaBytes Width
+    bool nullable = false; // scalar Nullable / TupleSchema.Nullable
+    bool variable = false; // TupleSchema.VariableLength
+    bool sorted = false;   // map pairs sorted by key (PackMapSorted)
+    std::string literal;   // K_MATCH
+    std::vector<int> kids; // emission order
+    std::string name;      // dotted field path
+    int col = -1;
+    int parent = -1;
+    int depth = 0;
+    int top = -1;
+};
+
+struct DeviceTables {
+    int device = -1;
+    void* block = nullptr;   // one allocation holding every table below
+    EncProgram enc{};
+    FixProgram fix{};
+    DecProgram dec{};
+};
+
+}  // namespace packos
+
+struct packos_schema {
+    int mode = 0;
+    std::vector<packos::Node> nodes;   // node 0 = K_ROOT (the chain)
+    std::vector<int> col_node;         // column -> node
+    std::vector<packos_column_info> col_info;
+    int n_top = 0;
+
+    // encode program (host copies)
+    std::vector<packos::EncItem> items;
+    std::vector<packos::EncHdr> hdrs;
+    std::vector<packos::EncCont> conts;
+    std::vector<uint8_t> lits;
+    bool has_var = false;        // any var-width leaf
+    bool has_nullable = false;   // any nullable leaf / container column
+    int64_t all_present_size = -1;  // blob size when every nullable is present (no var leaves)
+    bool all_present_overflow = false;
+
+    // fixed layout (valid when fix_ok)
+    bool fix_ok = false;
+    std::vector<packos::FixSeg> fsegs;
+    std::vector<uint32_t> fseg_index;
+    std::vector<packos::FixCol> fcols;
+    int fix_T = 0, fix_lds = 0, fix_chunks = 0;
+
+    // decode program
+    std::vector<packos::DecNode> dnodes;
+    std::vector<int32_t> dkids;
+
+    std::string describe;
+
+    std::mutex mu;
+    std::vector<packos::DeviceTables> dev;
+};
+
+namespace packos {
+// thread-local last error string
+void set_error(const std::string& m);
+int upload_tables(packos_schema* s, int device, DeviceTables** out);
+}  // namespace packos

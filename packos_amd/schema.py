@@ -75,7 +75,8 @@ class Schema:
         if self.kind != "string":
             raise TypeError("Match is defined on SchemaString")
         lit = expected.encode() if isinstance(expected, str) else bytes(expected)
-        return Schema("match", width=0, nullable=True, literal=lit)
+        # CheckFunc keeps the receiver's Width as the precheck hint (schema.go:1070-1130)
+        return Schema("match", width=self.width, nullable=self.width <= 0, literal=lit)
 
     def WithWidth(self, n: int) -> "Schema":
         if self.kind != "string":
@@ -143,7 +144,12 @@ class Schema:
                 return {"type": "string", "nullable": True}
             return {"type": "string"}
         if k == "match":
-            return {"type": "string", "exact": self.literal.decode("latin-1")}
+            d = {"type": "string", "exact": self.literal.decode("utf-8")}
+            if self.width > 0:
+                d["width"] = self.width
+            elif self.width < 0:
+                d["nullable"] = True
+            return d
         if k == "bytes":
             return {"type": "bytes", "width": self.width} if self.width > 0 else {"type": "bytes"}
         if k == "tuple":

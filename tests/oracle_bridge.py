@@ -112,7 +112,7 @@ class OracleSchema:
             elif k == "bytes":
                 nodes.extend([6, n.width, 0, 0])
             elif k == "match":
-                nodes.extend([7, len(lits), 0, 0])
+                nodes.extend([7, len(lits), n.width, 0])
                 lits.append(n.literal)
             elif k == "tuple":
                 nodes.extend([8, int(n.nullable), len(n.children), int(n.variable)])

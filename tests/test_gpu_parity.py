@@ -1,0 +1,263 @@
+"""HIP path vs CPU oracle, bit-exact (integer/byte work: no tolerance).
+
+Every test calls libpackos.so through the C ABI on cuda:0 and compares with
+the oracle on the same seeded inputs (oracle pinned by test_oracle_golden.py)
+or with the reference's golden bytes directly.
+"""
+import numpy as np
+import pytest
+
+import oracle_bridge as ob
+from golden_util import MODES, chain_of, load, unwrap
+from packos_amd.api import CompiledSchema, DeviceColumns, decode_batch, encode_batch, get_field_batch
+from packos_amd.columns import HostColumns
+from packos_amd.configs import CONFIGS, make_columns
+from packos_amd.schema import SChain, SInt16, SStringLen, SVariableString, STuple, SMap, SString
+from schema_gen import rand_chain, rand_rows
+
+pytestmark = pytest.mark.gpu
+G = load()
+
+
+def torch():
+    import torch as t
+    return t
+
+
+def gpu_encode(chain, hc, mode=0):
+    T = torch()
+    s = CompiledSchema(chain, mode)
+    dc = DeviceColumns.from_host(s, hc, "cuda:0")
+    r = encode_batch(s, dc)
+    T.cuda.synchronize()
+    arena = r.arena[: r.total].cpu().numpy()
+    offs = r.offsets.cpu().numpy().astype(np.uint64)
+    st = r.status.cpu().numpy().astype(np.uint32)
+    return arena, offs, st
+
+
+def assert_same_encoding(chain, hc, mode, what=""):
+    a0, o0, s0 = ob.encode(chain, hc, mode, nthreads=8)
+    a1, o1, s1 = gpu_encode(chain, hc, mode)
+    assert np.array_equal(o0, o1), f"{what}: offsets differ"
+    if not np.array_equal(a0, a1):
+        bad = int(np.nonzero(a0 != a1)[0][0])
+        blob = int(np.searchsorted(o0, bad, side="right") - 1)
+        raise AssertionError(f"{what}: first diff at byte {bad} (blob {blob}, +{bad - int(o0[blob])})")
+    assert np.array_equal(s0, s1), f"{what}: status differs"
+
+
+# --------------------------------------------------------------- golden ----
+@pytest.mark.parametrize("case", G["encode"], ids=[c["id"] for c in G["encode"]])
+def test_golden_encode(case):
+    chain = chain_of(case["schema"])
+    hc = HostColumns.from_rows(chain, [unwrap(case["row"])])
+    a, o, st = gpu_encode(chain, hc, MODES[case["mode"]])
+    assert bytes(a).hex() == case["hex"]
+    assert st[0] == 0
+
+
+@pytest.mark.parametrize("case", G["equal"], ids=[c["id"] for c in G["equal"]])
+def test_golden_cross_api(case):
+    outs = []
+    for v in case["variants"]:
+        chain = chain_of(v["schema"])
+        hc = HostColumns.from_rows(chain, [unwrap(case["row"])])
+        outs.append(bytes(gpu_encode(chain, hc, MODES[v["mode"]])[0]))
+    assert all(o == outs[0] for o in outs)
+
+
+# --------------------------------------------------------------- encode ----
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("seed", range(60))
+def test_random_schema_encode(seed, mode):
+    chain = rand_chain(seed)
+    hc = HostColumns.from_rows(chain, rand_rows(chain, 257, seed * 7 + 1))
+    assert_same_encoding(chain, hc, mode, f"seed {seed}")
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_random_fixed_schema_encode(seed):
+    # no var leaves, no nils: exercises the LDS-tiled fixed-layout kernel
+    chain = rand_chain(1000 + seed, allow_var=False, allow_null=False)
+    hc = HostColumns.from_rows(chain, rand_rows(chain, 1500, seed, nil_p=0.0))
+    hc.valid = [None] * len(hc.valid)
+    assert_same_encoding(chain, hc, 0, f"fixed seed {seed}")
+
+
+@pytest.mark.parametrize("n", [1, 2, 15, 16, 17, 63, 64, 65, 1000, 4097])
+def test_fixed_tail_tiles(n):
+    cfg = CONFIGS["M"]
+    assert_same_encoding(cfg.chain, make_columns(cfg, n=n), 0, f"M n={n}")
+
+
+@pytest.mark.parametrize("name,n", [("C1", 1000), ("C2", 100_003), ("M", 100_001), ("C3", 50_000),
+                                    ("C4", 65_537), ("C5", 20_000)])
+def test_configs_vs_oracle(name, n):
+    cfg = CONFIGS[name]
+    assert_same_encoding(cfg.chain, make_columns(cfg, n=n), cfg.mode, name)
+
+
+def test_overflow_13bit_and_large_blob():
+    # offsets >= 8192 are truncated exactly like typetags.EncodeHeader (Q1)
+    chain = SChain(SInt16, SVariableString(), SInt16, STuple(SVariableString(), SInt16))
+    rows = [[1, "x" * 9000, 2, ["y" * 10, 3]], [4, "short", 5, ["z" * 8200, 6]], [7, "", 8, None]]
+    hc = HostColumns.from_rows(chain, rows)
+    a0, o0, s0 = ob.encode(chain, hc, 0)
+    a1, o1, s1 = gpu_encode(chain, hc, 0)
+    assert np.array_equal(a0, a1) and np.array_equal(o0, o1) and np.array_equal(s0, s1)
+    assert s1[0] & 0x80000000 and s1[1] & 0x80000000 and s1[2] == 0
+
+
+def test_empty_batch_and_empty_chain():
+    T = torch()
+    s = CompiledSchema(SChain(), 0)
+    hc = HostColumns.from_rows(SChain(), [[], []])
+    a, o, st = gpu_encode(SChain(), hc, 0)
+    assert bytes(a) == bytes.fromhex("1000") * 2  # Pack() of an empty PutAccess
+    a, o, st = gpu_encode(SChain(), hc, 1)
+    assert a.size == 0  # packable.Pack() with no args
+    del s, T
+
+
+# --------------------------------------------------------------- decode ----
+def gpu_decode(chain, arena_np, offs_np, n):
+    T = torch()
+    s = CompiledSchema(chain, 0)
+    arena = T.from_numpy(arena_np if arena_np.size else np.zeros(16, np.uint8)).to("cuda:0")
+    offs = T.from_numpy(offs_np.astype(np.int64)).to("cuda:0")
+    out, st = decode_batch(s, arena, offs, n)
+    T.cuda.synchronize()
+    return out, st.cpu().numpy().astype(np.uint32)
+
+
+def assert_same_decode(chain, arena, offs, n, what=""):
+    o_out, o_st = ob.decode(chain, arena, offs, n, nthreads=8)
+    g_out, g_st = gpu_decode(chain, arena, offs, n)
+    if not np.array_equal(o_st, g_st):
+        bad = int(np.nonzero(o_st != g_st)[0][0])
+        raise AssertionError(f"{what}: status blob {bad}: oracle {o_st[bad]:#x} gpu {g_st[bad]:#x}")
+    for c in range(len(o_out.specs)):
+        for name in ("data", "valid", "start", "length"):
+            a = getattr(o_out, name)[c]
+            b = getattr(g_out, name)[c]
+            if a is None:
+                continue
+            bn = b.cpu().numpy()
+            if name == "start":
+                bn = bn.astype(np.uint64)
+            if name == "length":
+                bn = bn.astype(np.uint32)
+            assert np.array_equal(a[: bn.size], bn[: a.size]), f"{what}: column {c} {name}"
+    return g_st
+
+
+@pytest.mark.parametrize("case", G["decode"], ids=[c["id"] for c in G["decode"]])
+def test_golden_decode(case):
+    src = next((c for c in G["encode"] if c["id"] == case["input_from"]), None)
+    if src is not None:
+        blob = bytes.fromhex(src["hex"])
+    else:
+        eq = next(c for c in G["equal"] if c["id"] == case["input_from"])
+        v = eq["variants"][0]
+        ch = chain_of(v["schema"])
+        blob = bytes(ob.encode(ch, HostColumns.from_rows(ch, [unwrap(eq["row"])]), MODES[v["mode"]])[0])
+    chain = chain_of(case["schema"])
+    arena = np.frombuffer(blob, np.uint8).copy()
+    st = assert_same_decode(chain, arena, np.asarray([0, len(blob)], np.uint64), 1, case["id"])
+    assert int(st[0]) == case["expect_status"]
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_decode_roundtrip(seed):
+    chain = rand_chain(seed)
+    hc = HostColumns.from_rows(chain, rand_rows(chain, 300, seed + 99))
+    arena, offs, _ = ob.encode(chain, hc, 0)
+    st = assert_same_decode(chain, arena, offs, hc.n, f"seed {seed}")
+    assert (st == 0).all()
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_decode_corrupted(seed):
+    # flip header bytes / truncate blobs: every error code, position and panic
+    # must match the oracle's SeqGetAccess restatement
+    rng = np.random.default_rng(seed)
+    chain = rand_chain(seed)
+    hc = HostColumns.from_rows(chain, rand_rows(chain, 400, seed + 5))
+    arena, offs, _ = ob.encode(chain, hc, 0)
+    arena = arena.copy()
+    offs = offs.copy()
+    n = hc.n
+    for i in range(n):
+        a, b = int(offs[i]), int(offs[i + 1])
+        r = rng.random()
+        if r < 0.4 and b - a > 0:
+            k = int(rng.integers(0, min(b - a, 24)))
+            arena[a + k] = rng.integers(0, 256)
+        elif r < 0.5 and b - a > 0:
+            arena[a + int(rng.integers(0, b - a))] ^= 1 << int(rng.integers(0, 8))
+    # truncate some blobs by shifting their end offsets inward (keeps monotone)
+    cut = rng.random(n) < 0.1
+    ends = offs[1:].astype(np.int64)
+    starts = offs[:-1].astype(np.int64)
+    ends_cut = np.where(cut, starts + (ends - starts) // 2, ends)
+    # decode with an explicit [start, end) per blob: build a gapped arena
+    pieces, noffs = [], [0]
+    for i in range(n):
+        pieces.append(arena[starts[i]:ends_cut[i]])
+        noffs.append(noffs[-1] + int(ends_cut[i] - starts[i]))
+    arena2 = np.concatenate(pieces) if pieces else np.zeros(0, np.uint8)
+    assert_same_decode(chain, arena2, np.asarray(noffs, np.uint64), n, f"corrupt seed {seed}")
+
+
+@pytest.mark.parametrize("name,n", [("C3", 30_000), ("C4", 30_000), ("M", 30_000), ("C5", 5000)])
+def test_config_decode(name, n):
+    cfg = CONFIGS[name]
+    hc = make_columns(cfg, n=n)
+    arena, offs, _ = ob.encode(cfg.chain, hc, 0, nthreads=8)
+    st = assert_same_decode(cfg.chain, arena, offs, n, name)
+    assert (st == 0).all()
+
+
+# ------------------------------------------------------------ GetAccess ----
+@pytest.mark.parametrize("case", G["get"], ids=[c["id"] for c in G["get"]])
+def test_golden_get(case):
+    T = torch()
+    buf = np.frombuffer(bytes.fromhex(case["hex"]), np.uint8).copy()
+    arena = T.from_numpy(buf).to("cuda:0")
+    offs = T.tensor([0, buf.size], dtype=T.int64, device="cuda:0")
+    for q in case["queries"]:
+        s0, ln, tg, st = get_field_batch(arena, offs, 1, q["path"], q["tag"], q["width"])
+        T.cuda.synchronize()
+        assert int(st[0]) == 0
+        a = int(s0[0])
+        assert bytes(buf[a:a + int(ln[0])]).hex() == q["expect"]
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_random_get(seed):
+    T = torch()
+    rng = np.random.default_rng(seed)
+    chain = rand_chain(seed)
+    hc = HostColumns.from_rows(chain, rand_rows(chain, 200, seed))
+    arena, offs, _ = ob.encode(chain, hc, 0)
+    arena = arena.copy()
+    for i in range(0, hc.n, 3):  # corrupt a third of the blobs
+        a, b = int(offs[i]), int(offs[i + 1])
+        if b > a:
+            arena[a + int(rng.integers(0, min(8, b - a)))] = rng.integers(0, 256)
+    da = T.from_numpy(arena).to("cuda:0")
+    do = T.from_numpy(offs.astype(np.int64)).to("cuda:0")
+    for _ in range(12):
+        depth = int(rng.integers(1, 4))
+        path = [int(rng.integers(0, 6)) for _ in range(depth)]
+        tag = int(rng.choice([1, 3, 4, 5, 6, 7]))
+        width = int(rng.choice([-1, 1, 2, 4, 8]))
+        o = ob.get_field_batch(arena, offs, hc.n, path, tag, width)
+        g = get_field_batch(da, do, hc.n, path, tag, width)
+        T.cuda.synchronize()
+        gs = [x.cpu().numpy() for x in g]
+        assert np.array_equal(o[3], gs[3]), (path, tag, width)
+        okm = o[3] == 0
+        assert np.array_equal(o[0][okm], gs[0].astype(np.uint64)[okm])
+        assert np.array_equal(o[1][okm], gs[1].astype(np.uint32)[okm])

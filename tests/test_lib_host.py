@@ -1,0 +1,92 @@
+"""libpackos.so host-side checks (no GPU): the C ABI loads, exports every
+symbol include/packos.h declares, and the schema compiler's layout agrees
+with the oracle on blob sizes."""
+import ctypes as C
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle_bridge as ob
+from golden_util import MODES, chain_of, load, unwrap
+from packos_amd import _lib
+from packos_amd.api import CompiledSchema
+from packos_amd.columns import HostColumns
+from packos_amd.configs import CONFIGS, make_columns
+from schema_gen import rand_chain, rand_rows
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_exports_match_header():
+    hdr = open(os.path.join(ROOT, "include", "packos.h")).read()
+    declared = set(re.findall(r"\b(packos_[a-z_]+)\s*\(", hdr))
+    declared -= {"packos_column", "packos_schema"}
+    L = _lib.lib()
+    for name in sorted(declared):
+        assert hasattr(L, name), f"{name} declared in packos.h but not exported"
+    assert set(_lib.EXPORTED) == declared
+    assert L.packos_abi_version() == 1
+
+
+def test_schema_errors():
+    L = _lib.lib()
+    h = C.c_void_p()
+    assert L.packos_schema_compile(b"[{\"type\":\"email\"}]", 0, C.byref(h)) == -3
+    assert b"outside" in L.packos_last_error()
+    assert L.packos_schema_compile(b"[{\"type\":\"map\",\"schema\":[{\"type\":\"string\"}]}]", 0,
+                                   C.byref(h)) == -2
+    assert L.packos_schema_compile(b"[{\"type\":", 0, C.byref(h)) == -2
+    assert L.packos_schema_compile(b"[{\"type\":\"int16\",\"min\":0}]", 0, C.byref(h)) == -3
+    assert L.packos_schema_compile(b"[]", 7, C.byref(h)) == -1
+
+
+def test_config_blob_sizes():
+    assert CompiledSchema(CONFIGS["M"].chain).fixed_blob_size == 256
+    assert CompiledSchema(CONFIGS["C1"].chain).fixed_blob_size == 17
+    assert CompiledSchema(CONFIGS["C2"].chain).fixed_blob_size == 64
+    assert CompiledSchema(CONFIGS["C4"].chain).fixed_blob_size == 256
+    assert CompiledSchema(CONFIGS["C3"].chain).fixed_blob_size == -1
+    assert CompiledSchema(CONFIGS["C5"].chain).fixed_blob_size == -1
+
+
+def test_column_info_named():
+    s = CompiledSchema(CONFIGS["C3"].chain)
+    assert s.n_columns == 7
+    info = [s.column_info(c) for c in range(7)]
+    assert [i["name"] for i in info] == ["id", "ts", "score", "flag", "label", "code", "digest"]
+    assert info[4]["width"] == 0 and info[4]["kind"] == "string"
+    assert info[5]["width"] == 8
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("seed", range(40))
+def test_blob_sizes_vs_oracle(seed, mode):
+    chain = rand_chain(seed)
+    rows = rand_rows(chain, 20, seed + 1000)
+    hc = HostColumns.from_rows(chain, rows)
+    s = CompiledSchema(chain, mode)
+    _, offs, _ = ob.encode(chain, hc, mode)
+    sizes = np.diff(offs.astype(np.int64))
+    widths = hc.var_widths()
+    for i in range(hc.n):
+        valid = np.ones(len(hc.specs), np.uint8)
+        for c in range(len(hc.specs)):
+            if hc.valid[c] is not None:
+                valid[c] = hc.valid[c][i]
+        assert s.blob_size_host(widths[i], valid) == sizes[i], (seed, i, s.describe())
+
+
+def test_golden_schemas_compile():
+    g = load()
+    for case in g["encode"]:
+        s = CompiledSchema(chain_of(case["schema"]), MODES[case["mode"]])
+        hc = HostColumns.from_rows(s.chain, [unwrap(case["row"])])
+        widths = hc.var_widths()[0]
+        valid = np.ones(len(hc.specs), np.uint8)
+        for c in range(len(hc.specs)):
+            if hc.valid[c] is not None:
+                valid[c] = hc.valid[c][0]
+        assert s.blob_size_host(widths, valid) == len(case["hex"]) // 2, case["id"]
