@@ -191,6 +191,9 @@ int packos_encoded_size_batch(const packos_schema* s, const packos_column* cols,
  * schemas blobs that would end past out_capacity are not written and get
  * PACKOS_ERR_ENCODE in their status.                                         */
 #define PACKOS_ENC_OFFSETS_READY 1u
+/* testing/benchmark knob: use the general 4-blob-period fixed kernel even
+ * when the lane-invariant one applies                                        */
+#define PACKOS_ENC_FORCE_GENERIC 2u
 int packos_encode_batch(const packos_schema* s, const packos_column* cols, size_t n_blobs,
                         uint8_t* out_arena, uint64_t out_capacity, uint64_t* out_offsets,
                         uint32_t* status, void* workspace, size_t workspace_bytes,

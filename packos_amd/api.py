@@ -166,7 +166,7 @@ class EncodeResult:
 
 
 def encode_batch(schema: CompiledSchema, cols: DeviceColumns, want_offsets: bool = True,
-                 want_status: bool = True, out=None, stream=None) -> EncodeResult:
+                 want_status: bool = True, out=None, stream=None, flags: int = 0) -> EncodeResult:
     """Encode every blob of the batch (async on `stream`; one host sync for
     variable-size batches to size the arena)."""
     torch = _torch()
@@ -185,7 +185,7 @@ def encode_batch(schema: CompiledSchema, cols: DeviceColumns, want_offsets: bool
         offs = torch.empty(n + 1, dtype=torch.int64, device=dev) if want_offsets else None
         check(L.packos_encode_batch(schema.handle, arr, n, out.data_ptr(), out.numel(),
                                     None if offs is None else offs.data_ptr(),
-                                    None if status is None else status.data_ptr(), None, 0, 0, st),
+                                    None if status is None else status.data_ptr(), None, 0, flags, st),
               "packos_encode_batch")
         return EncodeResult(out, offs, status[:n] if status is not None else None, total, B)
     offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
@@ -206,8 +206,9 @@ class EncodePlan:
     """Pre-bound encode of a fixed-size batch into a preallocated arena: one
     C-ABI call per run() (what a serving loop or graph capture replays)."""
 
-    def __init__(self, schema: CompiledSchema, cols: DeviceColumns, out=None, stream=None):
+    def __init__(self, schema: CompiledSchema, cols: DeviceColumns, out=None, stream=None, flags: int = 0):
         torch = _torch()
+        self.flags = flags
         if cols.has_var() or cols.any_valid():
             raise ValueError("EncodePlan is for fixed-size batches")
         self.schema, self.cols = schema, cols
@@ -222,7 +223,8 @@ class EncodePlan:
     def run(self):
         st = _stream_ptr(self._stream)
         check(lib().packos_encode_batch(self.schema.handle, self._arr, self.cols.n, self.out.data_ptr(),
-                                        self.out.numel(), None, None, None, 0, 0, st), "packos_encode_batch")
+                                        self.out.numel(), None, None, None, 0, self.flags, st),
+              "packos_encode_batch")
         return self.out
 
 

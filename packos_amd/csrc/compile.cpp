@@ -427,6 +427,37 @@ struct Builder {
             }
         }
         s->fseg_index[B] = (uint32_t)s->fsegs.size();
+        // lane-invariant per-dword descriptors (blob-relative; B % 4 == 0 means
+        // no dword straddles two blobs)
+        s->fdw.clear();
+        if (B % 4 == 0) {
+            for (int64_t q = 0; q < B / 4; q++) {
+                DwDesc dd{};
+                int b = 0;
+                while (b < 4) {
+                    const BM& m = bm[4 * q + b];
+                    if (m.col < 0) {
+                        dd.cval |= (uint32_t)m.val << (8 * b);
+                        b++;
+                        continue;
+                    }
+                    int b1 = b + 1;
+                    while (b1 < 4) {
+                        const BM& m1 = bm[4 * q + b1];
+                        if (m1.col != m.col || m1.off != m.off + (b1 - b) || m.is_bool) break;
+                        b1++;
+                    }
+                    DwSeg sg{};
+                    sg.a = lds_of_col[m.col] + m.off - b;
+                    sg.w = (uint32_t)s->nodes[s->col_node[m.col]].width;
+                    for (int x = b; x < b1; x++) sg.mask |= 0xFFu << (8 * x);
+                    sg.flags = m.is_bool ? 1u : 0u;
+                    dd.seg[dd.nseg++] = sg;
+                    b = b1;
+                }
+                s->fdw.push_back(dd);
+            }
+        }
         // tile + descriptor tables must fit the 64 KiB dynamic LDS of one launch
         size_t lds_total = (size_t)s->fix_lds + ((size_t)(B + 1) * 4 + 15) / 16 * 16 + s->fsegs.size() * sizeof(FixSeg);
         s->fix_ok = lds_total <= 64 * 1024;

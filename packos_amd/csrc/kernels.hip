@@ -65,6 +65,98 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // =========================================================================
 // fixed-size encode
 // =========================================================================
+// Stage the tile's fixed input columns into LDS with 16-B coalesced loads.
+// Chunk k of the flattened tile maps to its column by a uniform select scan
+// over the (few) columns: no dependent loads.
+__device__ __forceinline__ void stage_tile(const FixProgram& P, const EncCols& cols, uint8_t* lds,
+                                           uint64_t blob0, uint32_t rows) {
+    const int tid = threadIdx.x;
+    const int total = P.total_chunks;
+    for (int k0 = 0; k0 < total; k0 += 4 * kBlock) {
+        uint4 v[4];
+        uint32_t dst[4];
+        bool ok[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + u * kBlock + tid;
+            const uint8_t* base = cols.data[P.fcols[0].col];
+            uint32_t width = P.fcols[0].width, lds_off = P.fcols[0].lds_off, cb = 0;
+            for (int g = 1; g < P.n_fcols; g++) {
+                const FixCol fc = P.fcols[g];   // uniform: scalar loads
+                const bool in = k >= (int)fc.chunk_begin;
+                base = in ? cols.data[fc.col] : base;
+                width = in ? fc.width : width;
+                lds_off = in ? fc.lds_off : lds_off;
+                cb = in ? fc.chunk_begin : cb;
+            }
+            ok[u] = false;
+            dst[u] = 0;
+            v[u] = make_uint4(0, 0, 0, 0);
+            if (k < total) {
+                const uint32_t byte = (uint32_t)(k - (int)cb) * 16u;
+                const uint32_t lim = rows * width;
+                const uint8_t* src = base + blob0 * width + byte;
+                dst[u] = lds_off + byte;
+                if (byte + 16 <= lim) {
+                    v[u] = *(const uint4*)src;
+                    ok[u] = true;
+                } else if (byte < lim) {
+                    uint32_t w[4] = {0, 0, 0, 0};
+                    for (uint32_t j = 0; j < lim - byte; j++) w[j >> 2] |= (uint32_t)src[j] << (8 * (j & 3));
+                    v[u] = make_uint4(w[0], w[1], w[2], w[3]);
+                    ok[u] = true;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (ok[u]) *(uint4*)(lds + dst[u]) = v[u];
+    }
+}
+
+__device__ __forceinline__ uint32_t lds_dword_at(const uint32_t* l32, uint32_t addr) {
+    const uint32_t lo = l32[addr >> 2], hi = l32[(addr >> 2) + 1];
+    return __builtin_amdgcn_alignbyte(hi, lo, addr & 3);
+}
+
+// Lane-invariant form (B % 4 == 0): thread t owns output dword q = t % (B/4)
+// of blobs s, s+R, s+2R ... of the tile; its byte sources sit in registers.
+__global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCols cols, uint8_t* __restrict__ out,
+                                                            uint64_t n, uint32_t* __restrict__ status,
+                                                            uint32_t st_val) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int T = P.T;
+    const uint32_t Q4 = (uint32_t)P.B >> 2;
+    const uint64_t blob0 = (uint64_t)blockIdx.x * (uint64_t)T;
+    const uint32_t rows = (uint32_t)min((uint64_t)T, n - blob0);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t q = tid % Q4, s = tid / Q4, R = kBlock / Q4;
+    DwDesc d;
+    if (s < R) d = P.dw[q];
+    stage_tile(P, cols, lds, blob0, rows);
+    __syncthreads();
+    if (s < R) {
+        const uint32_t* l32 = (const uint32_t*)lds;
+        uint32_t* o32 = (uint32_t*)(out + blob0 * (uint64_t)P.B) + q;
+        for (uint32_t j = s; j < rows; j += R) {
+            uint32_t v = d.cval;
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                if ((uint32_t)g < d.nseg) {
+                    uint32_t x = lds_dword_at(l32, (uint32_t)d.seg[g].a + j * d.seg[g].w) & d.seg[g].mask;
+                    if (d.seg[g].flags & 1u) x = x ? (d.seg[g].mask & 0x01010101u) : 0u;
+                    v |= x;
+                }
+            }
+            o32[(uint64_t)j * Q4] = v;
+        }
+    }
+    if (status)
+        for (uint32_t i = tid; i < rows; i += kBlock) status[blob0 + i] = st_val;
+}
+
+// General form (any B <= 1024): 16-B output chunks, per-dword segment lists
+// over a 4-blob period held in LDS.
 __global__ __launch_bounds__(kBlock) void k_encode_fixed(FixProgram P, EncCols cols,
                                                          uint8_t* __restrict__ out, uint64_t n,
                                                          uint32_t* __restrict__ status,
@@ -82,42 +174,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed(FixProgram P, EncCols c
     const uint32_t nsegs = P.seg_index[B];
     for (uint32_t k = tid; k <= B; k += kBlock) s_index[k] = P.seg_index[k];
     for (uint32_t k = tid; k < nsegs; k += kBlock) s_segs[k] = P.segs[k];
-
-    // ---- stage the tile's input rows: 16-B coalesced loads -> LDS
-    const int total = P.total_chunks;
-    for (int k0 = 0; k0 < total; k0 += 4 * kBlock) {
-        uint4 v[4];
-        uint32_t dst[4];
-        bool ok[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            int k = k0 + u * kBlock + tid;
-            ok[u] = false;
-            dst[u] = 0;
-            v[u] = make_uint4(0, 0, 0, 0);
-            if (k < total) {
-                int f = 0;
-                while (f + 1 < P.n_fcols && (int)P.fcols[f + 1].chunk_begin <= k) f++;
-                const FixCol fc = P.fcols[f];
-                const uint32_t byte = (uint32_t)(k - (int)fc.chunk_begin) * 16u;
-                const uint32_t lim = rows * fc.width;
-                const uint8_t* src = cols.data[fc.col] + blob0 * fc.width + byte;
-                dst[u] = fc.lds_off + byte;
-                if (byte + 16 <= lim) {
-                    v[u] = *(const uint4*)src;
-                    ok[u] = true;
-                } else if (byte < lim) {
-                    uint32_t w[4] = {0, 0, 0, 0};
-                    for (uint32_t j = 0; j < lim - byte; j++) w[j >> 2] |= (uint32_t)src[j] << (8 * (j & 3));
-                    v[u] = make_uint4(w[0], w[1], w[2], w[3]);
-                    ok[u] = true;
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-            if (ok[u]) *(uint4*)(lds + dst[u]) = v[u];
-    }
+    stage_tile(P, cols, lds, blob0, rows);
     __syncthreads();
 
     // ---- assemble 16-B output chunks
@@ -139,9 +196,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed(FixProgram P, EncCols c
                 if (g.stride4 == 0) {
                     v |= g.cval;
                 } else {
-                    const uint32_t addr = (uint32_t)g.a + per * g.stride4;
-                    const uint32_t lo = l32[addr >> 2], hi = l32[(addr >> 2) + 1];
-                    uint32_t x = __builtin_amdgcn_alignbyte(hi, lo, addr & 3) & g.mask;
+                    uint32_t x = lds_dword_at(l32, (uint32_t)g.a + per * g.stride4) & g.mask;
                     if (g.cval & 1u) x = x ? (g.mask & 0x01010101u) : 0u;
                     v |= x;
                 }
@@ -384,7 +439,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_var(EncProgram P, EncCols col
             if ((uint32_t)lane < total - done) out[o + done + lane] = dst[done + lane];
             __builtin_amdgcn_wave_barrier();
         }
-        if (status && lane == 0) status[i] = ovf ? PACKOS_STATUS_OVERFLOW13 : 0u;
+        const bool any_ovf = __ballot(ovf) != 0ull;
+        if (status && lane == 0) status[i] = any_ovf ? PACKOS_STATUS_OVERFLOW13 : 0u;
         // make sure no lane reuses the slot before every lane has read it
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -676,6 +732,7 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     size_t o_fsegs = put_bytes(blob, s->fsegs);
     size_t o_fidx = put_bytes(blob, s->fseg_index);
     size_t o_fcols = put_bytes(blob, s->fcols);
+    size_t o_fdw = put_bytes(blob, s->fdw);
     size_t o_dnodes = put_bytes(blob, s->dnodes);
     size_t o_dkids = put_bytes(blob, s->dkids);
     DeviceTables t;
@@ -694,6 +751,7 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     t.fix.segs = (const FixSeg*)(b + o_fsegs);
     t.fix.seg_index = (const uint32_t*)(b + o_fidx);
     t.fix.fcols = (const FixCol*)(b + o_fcols);
+    t.fix.dw = (const DwDesc*)(b + o_fdw);
     t.fix.B = (int)s->all_present_size;
     t.fix.T = s->fix_T;
     t.fix.n_fcols = (int)s->fcols.size();
@@ -799,10 +857,15 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
         for (const FixCol& fc : s->fcols) aligned = aligned && (((uintptr_t)ec.data[fc.col]) & 15) == 0;
         if (s->fix_ok && B >= 4 && aligned) {
             const uint64_t tiles = (n + s->fix_T - 1) / s->fix_T;
-            const size_t lds = (size_t)s->fix_lds + ((B + 1) * 4 + 15) / 16 * 16 + s->fsegs.size() * sizeof(FixSeg);
             const uint32_t stv = s->all_present_overflow ? PACKOS_STATUS_OVERFLOW13 : 0u;
-            hipLaunchKernelGGL(k_encode_fixed, dim3((unsigned)tiles), dim3(kBlock), lds, st, t->fix, ec, out,
-                               (uint64_t)n, status, stv);
+            if (!s->fdw.empty() && !(flags & PACKOS_ENC_FORCE_GENERIC)) {
+                hipLaunchKernelGGL(k_encode_fixed_dw, dim3((unsigned)tiles), dim3(kBlock), (size_t)s->fix_lds, st,
+                                   t->fix, ec, out, (uint64_t)n, status, stv);
+            } else {
+                const size_t lds = (size_t)s->fix_lds + ((B + 1) * 4 + 15) / 16 * 16 + s->fsegs.size() * sizeof(FixSeg);
+                hipLaunchKernelGGL(k_encode_fixed, dim3((unsigned)tiles), dim3(kBlock), lds, st, t->fix, ec, out,
+                                   (uint64_t)n, status, stv);
+            }
             HIP_TRY(hipGetLastError());
             return PACKOS_OK;
         }

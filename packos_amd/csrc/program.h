@@ -78,10 +78,27 @@ struct FixCol {
     uint32_t chunk_begin;// first 16-byte chunk of this column within the tile
 };
 
+// Lane-invariant form (B % 4 == 0): thread t always builds output dword
+// q = t % (B/4) of successive blobs, so its (at most 4) byte sources live in
+// registers for the whole tile.
+struct DwSeg {
+    int32_t a;        // LDS byte address of dword byte 0 for tile blob 0
+    uint32_t w;       // LDS bytes between consecutive blobs (column width)
+    uint32_t mask;    // byte-lane mask
+    uint32_t flags;   // bit0: bool normalise
+};
+struct DwDesc {
+    DwSeg seg[4];
+    uint32_t nseg;
+    uint32_t cval;    // constant bytes (header words, key literals)
+    uint32_t pad[2];
+};
+
 struct FixProgram {
     const FixSeg* segs;
     const uint32_t* seg_index;   // B+1 entries: segments of period-dword r
     const FixCol* fcols;
+    const DwDesc* dw;            // B/4 entries when B % 4 == 0
     int32_t B, T, n_fcols, lds_bytes, total_chunks, overflow;
 };
 

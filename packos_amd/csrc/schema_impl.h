@@ -56,6 +56,7 @@ struct packos_schema {
     std::vector<packos::FixSeg> fsegs;
     std::vector<uint32_t> fseg_index;
     std::vector<packos::FixCol> fcols;
+    std::vector<packos::DwDesc> fdw;   // lane-invariant descriptors (B % 4 == 0)
     int fix_T = 0, fix_lds = 0, fix_chunks = 0;
 
     // decode program
