@@ -43,6 +43,8 @@ constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kSlot = 8192 + 64;      // LDS staging bytes per wavefront (k_encode_var)
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ uint16_t enc_header(int64_t off, int tag) {
     return (uint16_t)((((uint64_t)off) << 3) & 0xFFFFu) | (uint16_t)(tag & 7);
 }
@@ -149,6 +151,68 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCol
                 }
             }
             o32[(uint64_t)j * Q4] = v;
+        }
+    }
+    if (status)
+        for (uint32_t i = tid; i < rows; i += kBlock) status[blob0 + i] = st_val;
+}
+
+// Lane-invariant form with the output tile re-staged in LDS so HBM sees only
+// 16-B-per-lane stores: dwords are built into registers (<= 16 per thread,
+// T*B <= 16 KiB), the input tile is retired by a barrier, the block writes the
+// output tile over it, then copies it out with global_store_dwordx4.
+template <bool NT>
+__global__ __launch_bounds__(kBlock) void k_encode_fixed_dw16(FixProgram P, EncCols cols, uint8_t* __restrict__ out,
+                                                              uint64_t n, uint32_t* __restrict__ status,
+                                                              uint32_t st_val) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int kMaxPer = 16;
+    const int T = P.T;
+    const uint32_t Q4 = (uint32_t)P.B >> 2;
+    const uint64_t blob0 = (uint64_t)blockIdx.x * (uint64_t)T;
+    const uint32_t rows = (uint32_t)min((uint64_t)T, n - blob0);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t q = tid % Q4, s = tid / Q4, R = kBlock / Q4;
+    DwDesc d;
+    if (s < R) d = P.dw[q];
+    stage_tile(P, cols, lds, blob0, rows);
+    __syncthreads();
+    uint32_t vals[kMaxPer];
+    const uint32_t* l32 = (const uint32_t*)lds;
+#pragma unroll
+    for (int m = 0; m < kMaxPer; m++) {
+        const uint32_t j = s + (uint32_t)m * R;
+        uint32_t v = d.cval;
+        if (s < R && j < rows) {
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                if ((uint32_t)g < d.nseg) {
+                    uint32_t x = lds_dword_at(l32, (uint32_t)d.seg[g].a + j * d.seg[g].w) & d.seg[g].mask;
+                    if (d.seg[g].flags & 1u) x = x ? (d.seg[g].mask & 0x01010101u) : 0u;
+                    v |= x;
+                }
+            }
+        }
+        vals[m] = v;
+    }
+    __syncthreads();
+    uint32_t* o_lds = (uint32_t*)lds;
+#pragma unroll
+    for (int m = 0; m < kMaxPer; m++) {
+        const uint32_t j = s + (uint32_t)m * R;
+        if (s < R && j < rows) o_lds[j * Q4 + q] = vals[m];
+    }
+    __syncthreads();
+    const uint32_t tile_bytes = rows * (uint32_t)P.B;
+    uint8_t* obase = out + blob0 * (uint64_t)P.B;
+    for (uint32_t c = tid; c * 16 < tile_bytes; c += kBlock) {
+        const uint32_t ob = 16 * c;
+        if (ob + 16 <= tile_bytes) {
+            const u32x4 v = *(const u32x4*)(lds + ob);
+            if (NT) __builtin_nontemporal_store(v, (u32x4*)(obase + ob));
+            else *(u32x4*)(obase + ob) = v;
+        } else {
+            for (uint32_t jb = ob; jb < tile_bytes; jb++) obase[jb] = lds[jb];
         }
     }
     if (status)
@@ -525,7 +589,12 @@ __global__ __launch_bounds__(kBlock) void k_decode(DecProgram P, DecCols cols, c
         const DecNode fn = P.nodes[f.node];
         if (f.k >= fn.nkids) {
             if (d == 0) break;
-            d--;  // container finished: Advance the parent past it
+            // container finished: mark it present, then Advance the parent past it
+            {
+                const DecNode cn = P.nodes[f.node];
+                if (cols.valid[cn.col]) cols.valid[cn.col][i] = 1;
+            }
+            d--;
             const int a = dseq_advance(st[d].q, arena);
             if (a) { err = a == 2 ? kPanic : 2; break; }
             st[d].k++;
@@ -539,7 +608,6 @@ __global__ __launch_bounds__(kBlock) void k_decode(DecProgram P, DecCols cols, c
             err = dprecheck(q, nd.tag, -1, nd.nullable, w);
             if (err) break;
             if (nd.kind == K_MAP && (nd.nkids & 1)) { err = 3; break; }
-            if (cols.valid[nd.col]) cols.valid[nd.col][i] = w != 0;
             if (w != 0) {
                 // PeekNestedSeq (seqget.go:105-121)
                 if (q.next_off - q.cur_off <= 0 || q.next_off > q.len) { err = 1; break; }
@@ -555,6 +623,7 @@ __global__ __launch_bounds__(kBlock) void k_decode(DecProgram P, DecCols cols, c
                 d++;
                 continue;
             }
+            if (cols.valid[nd.col]) cols.valid[nd.col][i] = 0;  // nil container
             const int a = dseq_advance(q, arena);
             if (a) { err = a == 2 ? kPanic : 2; break; }
             f.k++;
@@ -858,7 +927,17 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
         if (s->fix_ok && B >= 4 && aligned) {
             const uint64_t tiles = (n + s->fix_T - 1) / s->fix_T;
             const uint32_t stv = s->all_present_overflow ? PACKOS_STATUS_OVERFLOW13 : 0u;
-            if (!s->fdw.empty() && !(flags & PACKOS_ENC_FORCE_GENERIC)) {
+            const bool dw_ok = !s->fdw.empty() && !(flags & PACKOS_ENC_FORCE_GENERIC);
+            const bool dw16_ok = dw_ok && (uint64_t)s->fix_T * B <= 16 * 1024 && !(flags & PACKOS_ENC_FIXED_DWORD_STORES);
+            if (dw16_ok) {
+                const size_t lds = std::max<size_t>((size_t)s->fix_lds, (size_t)s->fix_T * B);
+                if (flags & PACKOS_ENC_FIXED_NT_STORES)
+                    hipLaunchKernelGGL(k_encode_fixed_dw16<true>, dim3((unsigned)tiles), dim3(kBlock), lds, st,
+                                       t->fix, ec, out, (uint64_t)n, status, stv);
+                else
+                    hipLaunchKernelGGL(k_encode_fixed_dw16<false>, dim3((unsigned)tiles), dim3(kBlock), lds, st,
+                                       t->fix, ec, out, (uint64_t)n, status, stv);
+            } else if (dw_ok) {
                 hipLaunchKernelGGL(k_encode_fixed_dw, dim3((unsigned)tiles), dim3(kBlock), (size_t)s->fix_lds, st,
                                    t->fix, ec, out, (uint64_t)n, status, stv);
             } else {

@@ -13,7 +13,7 @@ sys.path.insert(0, ROOT)
 from packos_amd.api import CompiledSchema, DeviceColumns, EncodePlan  # noqa: E402
 from packos_amd.configs import CONFIGS, algorithmic_bytes, make_columns  # noqa: E402
 
-VARIANTS = {"dw": 0, "generic": 2}
+VARIANTS = {"dw16": 0, "dw16nt": 8, "dw": 4, "generic": 2}
 
 
 def time_plan(plan, reps):
@@ -41,13 +41,13 @@ def main():
             p.run()
         torch.cuda.synchronize()
         outs = {k: p.out[: p.total].clone() for k, p in plans.items()}
-        same = all(torch.equal(outs["dw"], o) for o in outs.values())
+        same = all(torch.equal(outs["dw16"], o) for o in outs.values())
         times = {k: [] for k in plans}
         for _ in range(5):
             for k, p in plans.items():
                 times[k] += time_plan(p, 20)
-        alg = algorithmic_bytes(hc, plans["dw"].total, False)
-        res[name] = {"same_output": same, "B": plans["dw"].B, "n": n}
+        alg = algorithmic_bytes(hc, plans["dw16"].total, False)
+        res[name] = {"same_output": same, "B": plans["dw16"].B, "n": n}
         for k, t in times.items():
             med = float(np.median(t))
             res[name][k] = {"median_ms": round(med, 4), "min_ms": round(float(np.min(t)), 4),
@@ -57,3 +57,26 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def copy_ref(nbytes=256 << 20, reps=50):
+    """torch D2D copy of nbytes: the practical read+write streaming ceiling."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
+    b = torch.empty_like(a)
+    b.copy_(a)
+    st = torch.cuda.current_stream()
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        b.copy_(a)
+        e1.record(st)
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    med = float(np.median(ts))
+    print(json.dumps({"copy_ref": {"bytes_moved": 2 * nbytes, "median_ms": round(med, 4),
+                                   "GBs": round(2 * nbytes / med / 1e6, 1)}}), flush=True)
+
+
+if __name__ == "__main__" and os.environ.get("KBENCH_COPY", "1") == "1":
+    copy_ref()
