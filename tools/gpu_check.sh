@@ -1,10 +1,9 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 600 python tools/kbench.py M C2 C4 > gpurun_out/kbench.log 2>&1
-rc=$?; echo "kbench rc=$rc"; cat gpurun_out/kbench.log | grep -v amdgpu.ids
+timeout -k 10 300 ./tools/membench > gpurun_out/membench.log 2>&1
+rc=$?; echo "membench rc=$rc"; cat gpurun_out/membench.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
-rc=$?
-echo "pytest rc=$rc"
-tail -5 gpurun_out/pytest_gpu.log
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_M" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 3 --no-cpu > "$GRAFT_REPO_ROOT/gpurun_out/prof_M.log" 2>&1
+rc=$?; echo "rocprof rc=$rc"; tail -2 "$GRAFT_REPO_ROOT/gpurun_out/prof_M.log"
