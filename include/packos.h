@@ -194,10 +194,11 @@ int packos_encoded_size_batch(const packos_schema* s, const packos_column* cols,
 /* testing/benchmark knob: use the general 4-blob-period fixed kernel even
  * when the lane-invariant one applies                                        */
 #define PACKOS_ENC_FORCE_GENERIC 2u
-/* testing/benchmark knobs for the lane-invariant fixed kernel: store each
- * output dword directly (no LDS re-staging) / use non-temporal stores        */
-#define PACKOS_ENC_FIXED_DWORD_STORES 4u
-#define PACKOS_ENC_FIXED_NT_STORES    8u
+/* testing/benchmark knob: pick the fixed-layout kernel variant (0 = auto):
+ * 1..4 lane-invariant, dword stores {plain, NT stores, NT loads, NT both};
+ * 5..7 lane-invariant, LDS re-staged 16-B stores {plain, NT stores, NT both};
+ * 8 general 4-blob-period kernel                                             */
+#define PACKOS_ENC_FIXED_VARIANT(v) (((uint32_t)(v) & 0xFu) << 4)
 int packos_encode_batch(const packos_schema* s, const packos_column* cols, size_t n_blobs,
                         uint8_t* out_arena, uint64_t out_capacity, uint64_t* out_offsets,
                         uint32_t* status, void* workspace, size_t workspace_bytes,

@@ -45,6 +45,10 @@ constexpr int kSlot = 8192 + 64;      // LDS staging bytes per wavefront (k_enco
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// fixed-layout encode variant used when the caller does not pick one
+// (1..4: dword stores, 5..7: LDS re-staged 16-B stores; NT = non-temporal)
+constexpr int kDefaultFixedVariant = 1;
+
 __device__ __forceinline__ uint16_t enc_header(int64_t off, int tag) {
     return (uint16_t)((((uint64_t)off) << 3) & 0xFFFFu) | (uint16_t)(tag & 7);
 }
@@ -70,12 +74,13 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // Stage the tile's fixed input columns into LDS with 16-B coalesced loads.
 // Chunk k of the flattened tile maps to its column by a uniform select scan
 // over the (few) columns: no dependent loads.
+template <bool NTL>
 __device__ __forceinline__ void stage_tile(const FixProgram& P, const EncCols& cols, uint8_t* lds,
                                            uint64_t blob0, uint32_t rows) {
     const int tid = threadIdx.x;
     const int total = P.total_chunks;
     for (int k0 = 0; k0 < total; k0 += 4 * kBlock) {
-        uint4 v[4];
+        u32x4 v[4];
         uint32_t dst[4];
         bool ok[4];
 #pragma unroll
@@ -93,26 +98,26 @@ __device__ __forceinline__ void stage_tile(const FixProgram& P, const EncCols& c
             }
             ok[u] = false;
             dst[u] = 0;
-            v[u] = make_uint4(0, 0, 0, 0);
+            v[u] = u32x4{0, 0, 0, 0};
             if (k < total) {
                 const uint32_t byte = (uint32_t)(k - (int)cb) * 16u;
                 const uint32_t lim = rows * width;
                 const uint8_t* src = base + blob0 * width + byte;
                 dst[u] = lds_off + byte;
                 if (byte + 16 <= lim) {
-                    v[u] = *(const uint4*)src;
+                    v[u] = NTL ? __builtin_nontemporal_load((const u32x4*)src) : *(const u32x4*)src;
                     ok[u] = true;
                 } else if (byte < lim) {
                     uint32_t w[4] = {0, 0, 0, 0};
                     for (uint32_t j = 0; j < lim - byte; j++) w[j >> 2] |= (uint32_t)src[j] << (8 * (j & 3));
-                    v[u] = make_uint4(w[0], w[1], w[2], w[3]);
+                    v[u] = u32x4{w[0], w[1], w[2], w[3]};
                     ok[u] = true;
                 }
             }
         }
 #pragma unroll
         for (int u = 0; u < 4; u++)
-            if (ok[u]) *(uint4*)(lds + dst[u]) = v[u];
+            if (ok[u]) *(u32x4*)(lds + dst[u]) = v[u];
     }
 }
 
@@ -123,6 +128,7 @@ __device__ __forceinline__ uint32_t lds_dword_at(const uint32_t* l32, uint32_t a
 
 // Lane-invariant form (B % 4 == 0): thread t owns output dword q = t % (B/4)
 // of blobs s, s+R, s+2R ... of the tile; its byte sources sit in registers.
+template <bool NTL, bool NTS>
 __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCols cols, uint8_t* __restrict__ out,
                                                             uint64_t n, uint32_t* __restrict__ status,
                                                             uint32_t st_val) {
@@ -135,7 +141,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCol
     const uint32_t q = tid % Q4, s = tid / Q4, R = kBlock / Q4;
     DwDesc d;
     if (s < R) d = P.dw[q];
-    stage_tile(P, cols, lds, blob0, rows);
+    stage_tile<NTL>(P, cols, lds, blob0, rows);
     __syncthreads();
     if (s < R) {
         const uint32_t* l32 = (const uint32_t*)lds;
@@ -150,7 +156,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCol
                     v |= x;
                 }
             }
-            o32[(uint64_t)j * Q4] = v;
+            if (NTS) __builtin_nontemporal_store(v, o32 + (uint64_t)j * Q4);
+            else o32[(uint64_t)j * Q4] = v;
         }
     }
     if (status)
@@ -161,7 +168,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCol
 // 16-B-per-lane stores: dwords are built into registers (<= 16 per thread,
 // T*B <= 16 KiB), the input tile is retired by a barrier, the block writes the
 // output tile over it, then copies it out with global_store_dwordx4.
-template <bool NT>
+template <bool NTL, bool NT>
 __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw16(FixProgram P, EncCols cols, uint8_t* __restrict__ out,
                                                               uint64_t n, uint32_t* __restrict__ status,
                                                               uint32_t st_val) {
@@ -175,7 +182,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw16(FixProgram P, EncC
     const uint32_t q = tid % Q4, s = tid / Q4, R = kBlock / Q4;
     DwDesc d;
     if (s < R) d = P.dw[q];
-    stage_tile(P, cols, lds, blob0, rows);
+    stage_tile<NTL>(P, cols, lds, blob0, rows);
     __syncthreads();
     uint32_t vals[kMaxPer];
     const uint32_t* l32 = (const uint32_t*)lds;
@@ -238,7 +245,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed(FixProgram P, EncCols c
     const uint32_t nsegs = P.seg_index[B];
     for (uint32_t k = tid; k <= B; k += kBlock) s_index[k] = P.seg_index[k];
     for (uint32_t k = tid; k < nsegs; k += kBlock) s_segs[k] = P.segs[k];
-    stage_tile(P, cols, lds, blob0, rows);
+    stage_tile<false>(P, cols, lds, blob0, rows);
     __syncthreads();
 
     // ---- assemble 16-B output chunks
@@ -927,20 +934,26 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
         if (s->fix_ok && B >= 4 && aligned) {
             const uint64_t tiles = (n + s->fix_T - 1) / s->fix_T;
             const uint32_t stv = s->all_present_overflow ? PACKOS_STATUS_OVERFLOW13 : 0u;
-            const bool dw_ok = !s->fdw.empty() && !(flags & PACKOS_ENC_FORCE_GENERIC);
-            const bool dw16_ok = dw_ok && (uint64_t)s->fix_T * B <= 16 * 1024 && !(flags & PACKOS_ENC_FIXED_DWORD_STORES);
-            if (dw16_ok) {
-                const size_t lds = std::max<size_t>((size_t)s->fix_lds, (size_t)s->fix_T * B);
-                if (flags & PACKOS_ENC_FIXED_NT_STORES)
-                    hipLaunchKernelGGL(k_encode_fixed_dw16<true>, dim3((unsigned)tiles), dim3(kBlock), lds, st,
-                                       t->fix, ec, out, (uint64_t)n, status, stv);
-                else
-                    hipLaunchKernelGGL(k_encode_fixed_dw16<false>, dim3((unsigned)tiles), dim3(kBlock), lds, st,
-                                       t->fix, ec, out, (uint64_t)n, status, stv);
-            } else if (dw_ok) {
-                hipLaunchKernelGGL(k_encode_fixed_dw, dim3((unsigned)tiles), dim3(kBlock), (size_t)s->fix_lds, st,
-                                   t->fix, ec, out, (uint64_t)n, status, stv);
-            } else {
+            int variant = (int)((flags >> 4) & 0xF);
+            if (flags & PACKOS_ENC_FORCE_GENERIC) variant = 8;
+            const bool dw_ok = !s->fdw.empty();
+            const bool dw16_ok = dw_ok && (uint64_t)s->fix_T * B <= 16 * 1024;
+            if (variant == 0) variant = dw_ok ? kDefaultFixedVariant : 8;
+            if ((variant >= 5 && variant <= 7 && !dw16_ok) || (variant <= 4 && !dw_ok)) variant = 8;
+            const dim3 g((unsigned)tiles), b(kBlock);
+            const size_t lds_dw = (size_t)s->fix_lds;
+            const size_t lds_dw16 = std::max<size_t>((size_t)s->fix_lds, (size_t)s->fix_T * B);
+            switch (variant) {
+                case 1: hipLaunchKernelGGL((k_encode_fixed_dw<false, false>), g, b, lds_dw, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
+                case 2: hipLaunchKernelGGL((k_encode_fixed_dw<false, true>), g, b, lds_dw, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
+                case 3: hipLaunchKernelGGL((k_encode_fixed_dw<true, false>), g, b, lds_dw, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
+                case 4: hipLaunchKernelGGL((k_encode_fixed_dw<true, true>), g, b, lds_dw, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
+                case 5: hipLaunchKernelGGL((k_encode_fixed_dw16<false, false>), g, b, lds_dw16, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
+                case 6: hipLaunchKernelGGL((k_encode_fixed_dw16<false, true>), g, b, lds_dw16, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
+                case 7: hipLaunchKernelGGL((k_encode_fixed_dw16<true, true>), g, b, lds_dw16, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
+                default: variant = 8; break;
+            }
+            if (variant == 8) {
                 const size_t lds = (size_t)s->fix_lds + ((B + 1) * 4 + 15) / 16 * 16 + s->fsegs.size() * sizeof(FixSeg);
                 hipLaunchKernelGGL(k_encode_fixed, dim3((unsigned)tiles), dim3(kBlock), lds, st, t->fix, ec, out,
                                    (uint64_t)n, status, stv);

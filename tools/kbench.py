@@ -13,7 +13,8 @@ sys.path.insert(0, ROOT)
 from packos_amd.api import CompiledSchema, DeviceColumns, EncodePlan  # noqa: E402
 from packos_amd.configs import CONFIGS, algorithmic_bytes, make_columns  # noqa: E402
 
-VARIANTS = {"dw16": 0, "dw16nt": 8, "dw": 4, "generic": 2}
+VARIANTS = {"v1_dw": 1 << 4, "v2_dw_nts": 2 << 4, "v3_dw_ntl": 3 << 4, "v4_dw_ntls": 4 << 4,
+            "v5_dw16": 5 << 4, "v6_dw16_nts": 6 << 4, "v7_dw16_ntls": 7 << 4, "v8_generic": 8 << 4}
 
 
 def time_plan(plan, reps):
@@ -41,13 +42,13 @@ def main():
             p.run()
         torch.cuda.synchronize()
         outs = {k: p.out[: p.total].clone() for k, p in plans.items()}
-        same = all(torch.equal(outs["dw16"], o) for o in outs.values())
+        same = all(torch.equal(outs["v1_dw"], o) for o in outs.values())
         times = {k: [] for k in plans}
         for _ in range(5):
             for k, p in plans.items():
                 times[k] += time_plan(p, 20)
-        alg = algorithmic_bytes(hc, plans["dw16"].total, False)
-        res[name] = {"same_output": same, "B": plans["dw16"].B, "n": n}
+        alg = algorithmic_bytes(hc, plans["v1_dw"].total, False)
+        res[name] = {"same_output": same, "B": plans["v1_dw"].B, "n": n}
         for k, t in times.items():
             med = float(np.median(t))
             res[name][k] = {"median_ms": round(med, 4), "min_ms": round(float(np.min(t)), 4),
