@@ -354,7 +354,10 @@ struct Builder {
         if (B <= 0 || B > 1024) return;  // large fixed blobs use the general kernel
 
         // tile size: T blobs (multiple of 16 so tile in/out are whole 16-B chunks)
-        int T = (int)((16384 / B) / 16 * 16);
+        // ~16 KiB of output per tile (env PACKOS_TILE_BYTES overrides, tuning only)
+        int64_t tile_bytes = 16384;
+        if (const char* e = getenv("PACKOS_TILE_BYTES")) tile_bytes = std::max<int64_t>(1024, atoll(e));
+        int T = (int)((tile_bytes / B) / 16 * 16);
         if (T < 16) T = 16;
         if (T > 1024) T = 1024;
         s->fix_T = T;

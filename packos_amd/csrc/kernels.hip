@@ -128,40 +128,46 @@ __device__ __forceinline__ uint32_t lds_dword_at(const uint32_t* l32, uint32_t a
 
 // Lane-invariant form (B % 4 == 0): thread t owns output dword q = t % (B/4)
 // of blobs s, s+R, s+2R ... of the tile; its byte sources sit in registers.
-template <bool NTL, bool NTS>
+// PERSIST: a grid of ~CUs x 8 workgroups walks the tiles (descriptors loaded
+// once per workgroup instead of once per tile).
+template <bool NTL, bool NTS, bool PERSIST = false>
 __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCols cols, uint8_t* __restrict__ out,
                                                             uint64_t n, uint32_t* __restrict__ status,
                                                             uint32_t st_val) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int T = P.T;
     const uint32_t Q4 = (uint32_t)P.B >> 2;
-    const uint64_t blob0 = (uint64_t)blockIdx.x * (uint64_t)T;
-    const uint32_t rows = (uint32_t)min((uint64_t)T, n - blob0);
     const uint32_t tid = threadIdx.x;
     const uint32_t q = tid % Q4, s = tid / Q4, R = kBlock / Q4;
+    const uint64_t ntiles = (n + T - 1) / T;
     DwDesc d;
     if (s < R) d = P.dw[q];
-    stage_tile<NTL>(P, cols, lds, blob0, rows);
-    __syncthreads();
-    if (s < R) {
-        const uint32_t* l32 = (const uint32_t*)lds;
-        uint32_t* o32 = (uint32_t*)(out + blob0 * (uint64_t)P.B) + q;
-        for (uint32_t j = s; j < rows; j += R) {
-            uint32_t v = d.cval;
+    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += PERSIST ? gridDim.x : ntiles) {
+        const uint64_t blob0 = tile * (uint64_t)T;
+        const uint32_t rows = (uint32_t)min((uint64_t)T, n - blob0);
+        if (PERSIST) __syncthreads();  // previous tile's LDS reads are done
+        stage_tile<NTL>(P, cols, lds, blob0, rows);
+        __syncthreads();
+        if (s < R) {
+            const uint32_t* l32 = (const uint32_t*)lds;
+            uint32_t* o32 = (uint32_t*)(out + blob0 * (uint64_t)P.B) + q;
+            for (uint32_t j = s; j < rows; j += R) {
+                uint32_t v = d.cval;
 #pragma unroll
-            for (int g = 0; g < 4; g++) {
-                if ((uint32_t)g < d.nseg) {
-                    uint32_t x = lds_dword_at(l32, (uint32_t)d.seg[g].a + j * d.seg[g].w) & d.seg[g].mask;
-                    if (d.seg[g].flags & 1u) x = x ? (d.seg[g].mask & 0x01010101u) : 0u;
-                    v |= x;
+                for (int g = 0; g < 4; g++) {
+                    if ((uint32_t)g < d.nseg) {
+                        uint32_t x = lds_dword_at(l32, (uint32_t)d.seg[g].a + j * d.seg[g].w) & d.seg[g].mask;
+                        if (d.seg[g].flags & 1u) x = x ? (d.seg[g].mask & 0x01010101u) : 0u;
+                        v |= x;
+                    }
                 }
+                if (NTS) __builtin_nontemporal_store(v, o32 + (uint64_t)j * Q4);
+                else o32[(uint64_t)j * Q4] = v;
             }
-            if (NTS) __builtin_nontemporal_store(v, o32 + (uint64_t)j * Q4);
-            else o32[(uint64_t)j * Q4] = v;
         }
+        if (status)
+            for (uint32_t i = tid; i < rows; i += kBlock) status[blob0 + i] = st_val;
     }
-    if (status)
-        for (uint32_t i = tid; i < rows; i += kBlock) status[blob0 + i] = st_val;
 }
 
 // Lane-invariant form with the output tile re-staged in LDS so HBM sees only
@@ -766,6 +772,17 @@ int current_device(int* dev) {
     return PACKOS_OK;
 }
 
+int cu_count(int dev) {
+    static int cache[64] = {0};
+    if (dev < 0 || dev >= 64) return 256;
+    if (!cache[dev]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        cache[dev] = v;
+    }
+    return cache[dev];
+}
+
 int fill_enc_cols(const packos_schema* s, const packos_column* cols, EncCols& ec, bool* any_nil) {
     memset(&ec, 0, sizeof(ec));
     *any_nil = false;
@@ -939,7 +956,7 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
             const bool dw_ok = !s->fdw.empty();
             const bool dw16_ok = dw_ok && (uint64_t)s->fix_T * B <= 16 * 1024;
             if (variant == 0) variant = dw_ok ? kDefaultFixedVariant : 8;
-            if ((variant >= 5 && variant <= 7 && !dw16_ok) || (variant <= 4 && !dw_ok)) variant = 8;
+            if ((variant >= 5 && variant <= 7 && !dw16_ok) || ((variant <= 4 || variant >= 9) && !dw_ok)) variant = 8;
             const dim3 g((unsigned)tiles), b(kBlock);
             const size_t lds_dw = (size_t)s->fix_lds;
             const size_t lds_dw16 = std::max<size_t>((size_t)s->fix_lds, (size_t)s->fix_T * B);
@@ -951,6 +968,14 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
                 case 5: hipLaunchKernelGGL((k_encode_fixed_dw16<false, false>), g, b, lds_dw16, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
                 case 6: hipLaunchKernelGGL((k_encode_fixed_dw16<false, true>), g, b, lds_dw16, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
                 case 7: hipLaunchKernelGGL((k_encode_fixed_dw16<true, true>), g, b, lds_dw16, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
+                case 9: case 10: {
+                    const dim3 gp((unsigned)std::min<uint64_t>(tiles, (uint64_t)cu_count(dev) * 8));
+                    if (variant == 9)
+                        hipLaunchKernelGGL((k_encode_fixed_dw<false, true, true>), gp, b, lds_dw, st, t->fix, ec, out, (uint64_t)n, status, stv);
+                    else
+                        hipLaunchKernelGGL((k_encode_fixed_dw<true, true, true>), gp, b, lds_dw, st, t->fix, ec, out, (uint64_t)n, status, stv);
+                    break;
+                }
                 default: variant = 8; break;
             }
             if (variant == 8) {

@@ -13,8 +13,9 @@ sys.path.insert(0, ROOT)
 from packos_amd.api import CompiledSchema, DeviceColumns, EncodePlan  # noqa: E402
 from packos_amd.configs import CONFIGS, algorithmic_bytes, make_columns  # noqa: E402
 
-VARIANTS = {"v1_dw": 1 << 4, "v2_dw_nts": 2 << 4, "v3_dw_ntl": 3 << 4, "v4_dw_ntls": 4 << 4,
-            "v5_dw16": 5 << 4, "v6_dw16_nts": 6 << 4, "v7_dw16_ntls": 7 << 4, "v8_generic": 8 << 4}
+VARIANTS = {k: int(v) << 4 for k, v in (x.split("=") for x in os.environ.get(
+    "KBENCH_VARIANTS", "v1=1,v2=2,v4=4,v9=9,v10=10,v8=8").split(","))}
+TILES = [int(x) for x in os.environ.get("KBENCH_TILES", "16384").split(",")]
 
 
 def time_plan(plan, reps):
@@ -35,20 +36,25 @@ def main():
         cfg = CONFIGS[name]
         n = cfg.n if name != "C4" else cfg.n
         hc = make_columns(cfg, n=n)
-        s = CompiledSchema(cfg.chain, cfg.mode)
-        dc = DeviceColumns.from_host(s, hc, "cuda:0")
-        plans = {k: EncodePlan(s, dc, flags=f) for k, f in VARIANTS.items()}
+        plans = {}
+        for tb in TILES:
+            os.environ["PACKOS_TILE_BYTES"] = str(tb)
+            s = CompiledSchema(cfg.chain, cfg.mode)
+            dc = DeviceColumns.from_host(s, hc, "cuda:0")
+            for k, f in VARIANTS.items():
+                plans[f"{k}_t{tb // 1024}k"] = EncodePlan(s, dc, flags=f)
+        first = next(iter(plans))
         for p in plans.values():
             p.run()
         torch.cuda.synchronize()
         outs = {k: p.out[: p.total].clone() for k, p in plans.items()}
-        same = all(torch.equal(outs["v1_dw"], o) for o in outs.values())
+        same = all(torch.equal(outs[first], o) for o in outs.values())
         times = {k: [] for k in plans}
         for _ in range(5):
             for k, p in plans.items():
                 times[k] += time_plan(p, 20)
-        alg = algorithmic_bytes(hc, plans["v1_dw"].total, False)
-        res[name] = {"same_output": same, "B": plans["v1_dw"].B, "n": n}
+        alg = algorithmic_bytes(hc, plans[first].total, False)
+        res[name] = {"same_output": same, "B": plans[first].B, "n": n}
         for k, t in times.items():
             med = float(np.median(t))
             res[name][k] = {"median_ms": round(med, 4), "min_ms": round(float(np.min(t)), 4),
