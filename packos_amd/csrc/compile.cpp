@@ -356,7 +356,8 @@ struct Builder {
         // tile size: T blobs (multiple of 16 so tile in/out are whole 16-B chunks)
         // ~16 KiB of output per tile (env PACKOS_TILE_BYTES overrides, tuning only)
         int64_t tile_bytes = 16384;
-        if (const char* e = getenv("PACKOS_TILE_BYTES")) tile_bytes = std::max<int64_t>(1024, atoll(e));
+        if (const char* e = getenv("PACKOS_TILE_BYTES"))
+            tile_bytes = std::min<int64_t>(16384, std::max<int64_t>(1024, atoll(e)));  // staging plan holds <= 16 KiB
         int T = (int)((tile_bytes / B) / 16 * 16);
         if (T < 16) T = 16;
         if (T > 1024) T = 1024;
