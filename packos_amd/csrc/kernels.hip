@@ -74,77 +74,50 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // Stage the tile's fixed input columns into LDS with 16-B coalesced loads.
 // A tile holds at most 16 KiB of input (T*B <= 16 KiB and the input bytes of
 // a blob never exceed its size), i.e. <= 1024 16-B chunks = 4 per thread.
-// Which column each of a thread's 4 chunks comes from is tile-invariant, so it
-// is resolved once (StagePlan) and every tile then issues its 4 loads
-// back-to-back with no dependent lookups in between.
+// Each chunk's column is found by a uniform walk over the (few) columns with
+// scalar loads and per-lane selects — no dependent vector loads — and its
+// 16-B load is issued at once, so a thread's 4 loads are in flight together.
+// (Precomputing this plan once per workgroup costs ~20 VGPRs and halves
+// occupancy; recomputing it is a handful of SALU/VALU ops per tile.)
 constexpr int kStageSlots = 4;
-struct StagePlan {
-    const uint8_t* src[kStageSlots];  // column base + byte offset within the tile region
-    uint32_t w[kStageSlots];          // column width (0 = slot unused)
-    uint32_t dst[kStageSlots];        // LDS destination
-    uint32_t byte[kStageSlots];       // byte offset within the column's tile region
-};
-
-__device__ __forceinline__ StagePlan make_stage_plan(const FixProgram& P, const EncCols& cols) {
-    StagePlan sp;
-    const int tid = threadIdx.x;
-#pragma unroll
-    for (int u = 0; u < kStageSlots; u++) {
-        sp.w[u] = 0; sp.dst[u] = 0; sp.byte[u] = 0; sp.src[u] = nullptr;
-    }
-    // uniform walk over the columns (scalar loads); each lane keeps the last
-    // column whose chunk range starts at or before each of its chunks
-    for (int g = 0; g < P.n_fcols; g++) {
-        const FixCol fc = P.fcols[g];
-        const uint8_t* base = cols.data[fc.col];
-#pragma unroll
-        for (int u = 0; u < kStageSlots; u++) {
-            const int k = u * kBlock + tid;
-            if (k >= (int)fc.chunk_begin && k < P.total_chunks) {
-                const uint32_t byte = (uint32_t)(k - (int)fc.chunk_begin) * 16u;
-                sp.src[u] = base + byte;
-                sp.w[u] = fc.width;
-                sp.dst[u] = fc.lds_off + byte;
-                sp.byte[u] = byte;
-            }
-        }
-    }
-    return sp;
-}
 
 template <bool NTL>
-__device__ __forceinline__ void stage_tile(const StagePlan& sp, uint8_t* lds, uint64_t blob0, uint32_t rows,
-                                           uint32_t T) {
+__device__ __forceinline__ void stage_tile(const FixProgram& P, const EncCols& cols, uint8_t* lds, uint64_t blob0,
+                                           uint32_t rows, uint32_t T) {
+    (void)T;
+    const int tid = threadIdx.x;
     u32x4 v[kStageSlots];
+    uint32_t dst[kStageSlots];
     bool ok[kStageSlots];
-    if (rows == T) {  // full tile (uniform): every used slot is a whole 16-B chunk, no branches
-#pragma unroll
-        for (int u = 0; u < kStageSlots; u++) {
-            const uint8_t* src = sp.src[u] + blob0 * sp.w[u];
-            if (sp.w[u]) v[u] = NTL ? __builtin_nontemporal_load((const u32x4*)src) : *(const u32x4*)src;
-        }
-#pragma unroll
-        for (int u = 0; u < kStageSlots; u++)
-            if (sp.w[u]) *(u32x4*)(lds + sp.dst[u]) = v[u];
-        return;
-    }
 #pragma unroll
     for (int u = 0; u < kStageSlots; u++) {
-        const uint32_t lim = rows * sp.w[u];
-        const uint8_t* src = sp.src[u] + blob0 * sp.w[u];
-        ok[u] = sp.byte[u] < lim;
-        v[u] = u32x4{0, 0, 0, 0};
-        if (sp.byte[u] + 16 <= lim) {
+        const int k = u * kBlock + tid;
+        const uint8_t* base = nullptr;
+        uint32_t w = 0, lo = 0, cb = 0;
+        for (int g = 0; g < P.n_fcols; g++) {
+            const FixCol fc = P.fcols[g];
+            const bool in = k >= (int)fc.chunk_begin;
+            base = in ? cols.data[fc.col] : base;
+            w = in ? fc.width : w;
+            lo = in ? fc.lds_off : lo;
+            cb = in ? fc.chunk_begin : cb;
+        }
+        const uint32_t byte = (uint32_t)(k - (int)cb) * 16u;
+        const uint32_t lim = k < P.total_chunks ? rows * w : 0u;
+        const uint8_t* src = base + blob0 * w + byte;
+        dst[u] = lo + byte;
+        ok[u] = byte < lim;
+        if (byte + 16 <= lim) {
             v[u] = NTL ? __builtin_nontemporal_load((const u32x4*)src) : *(const u32x4*)src;
         } else if (ok[u]) {  // last, partial chunk of the final tile
-            uint32_t w[4] = {0, 0, 0, 0};
-            for (uint32_t j = 0; j < lim - sp.byte[u]; j++) w[j >> 2] |= (uint32_t)src[j] << (8 * (j & 3));
-            v[u] = u32x4{w[0], w[1], w[2], w[3]};
+            uint32_t w4[4] = {0, 0, 0, 0};
+            for (uint32_t j = 0; j < lim - byte; j++) w4[j >> 2] |= (uint32_t)src[j] << (8 * (j & 3));
+            v[u] = u32x4{w4[0], w4[1], w4[2], w4[3]};
         }
     }
 #pragma unroll
     for (int u = 0; u < kStageSlots; u++)
-        if (ok[u]) *(u32x4*)(lds + sp.dst[u]) = v[u];
+        if (ok[u]) *(u32x4*)(lds + dst[u]) = v[u];
 }
 
 __device__ __forceinline__ uint32_t lds_dword_at(const uint32_t* l32, uint32_t addr) {
@@ -168,12 +141,11 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCol
     const uint64_t ntiles = (n + T - 1) / T;
     DwDesc d;
     if (s < R) d = P.dw[q];
-    const StagePlan sp = make_stage_plan(P, cols);
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += PERSIST ? gridDim.x : ntiles) {
         const uint64_t blob0 = tile * (uint64_t)T;
         const uint32_t rows = (uint32_t)min((uint64_t)T, n - blob0);
         if (PERSIST) __syncthreads();  // previous tile's LDS reads are done
-        stage_tile<NTL>(sp, lds, blob0, rows, (uint32_t)T);
+        stage_tile<NTL>(P, cols, lds, blob0, rows, (uint32_t)T);
         __syncthreads();
         if (s < R) {
             const uint32_t* l32 = (const uint32_t*)lds;
@@ -215,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw16(FixProgram P, EncC
     const uint32_t q = tid % Q4, s = tid / Q4, R = kBlock / Q4;
     DwDesc d;
     if (s < R) d = P.dw[q];
-    stage_tile<NTL>(make_stage_plan(P, cols), lds, blob0, rows, (uint32_t)T);
+    stage_tile<NTL>(P, cols, lds, blob0, rows, (uint32_t)T);
     __syncthreads();
     uint32_t vals[kMaxPer];
     const uint32_t* l32 = (const uint32_t*)lds;
@@ -278,7 +250,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed(FixProgram P, EncCols c
     const uint32_t nsegs = P.seg_index[B];
     for (uint32_t k = tid; k <= B; k += kBlock) s_index[k] = P.seg_index[k];
     for (uint32_t k = tid; k < nsegs; k += kBlock) s_segs[k] = P.segs[k];
-    stage_tile<false>(make_stage_plan(P, cols), lds, blob0, rows, (uint32_t)T);
+    stage_tile<false>(P, cols, lds, blob0, rows, (uint32_t)T);
     __syncthreads();
 
     // ---- assemble 16-B output chunks
