@@ -75,17 +75,45 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // A tile holds at most 16 KiB of input (T*B <= 16 KiB and the input bytes of
 // a blob never exceed its size), i.e. <= 1024 16-B chunks = 4 per thread.
 // Each chunk's column is found by a uniform walk over the (few) columns with
-// scalar loads and per-lane selects — no dependent vector loads — and its
-// 16-B load is issued at once, so a thread's 4 loads are in flight together.
-// (Precomputing this plan once per workgroup costs ~20 VGPRs and halves
-// occupancy; recomputing it is a handful of SALU/VALU ops per tile.)
+// per-lane selects, reading the column table from an LDS copy (fcols_to_lds):
+// had the table come from global memory, every lookup's s_waitcnt vmcnt(0)
+// would also wait for the previous slot's in-flight data load and serialise
+// them.  A thread's 4 loads are thus in flight together.  (Precomputing this
+// plan once per workgroup costs ~20 VGPRs and halves occupancy; recomputing
+// it is a handful of VALU ops per tile.)
 constexpr int kStageSlots = 4;
+
+// The column base pointers come from LDS, so the compiler no longer knows they
+// address global memory and would emit flat loads (which need vmcnt(0) AND
+// lgkmcnt(0) waits).  Cast back to the global address space explicitly.
+typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+template <bool NT>
+__device__ __forceinline__ u32x4 gload16(const uint8_t* p) {
+    const g_u32x4* gp = (const g_u32x4*)p;
+    return NT ? __builtin_nontemporal_load(gp) : *gp;
+}
+
+struct LFix {                 // LDS copy of a FixCol with its column base resolved
+    const uint8_t* base;
+    uint32_t width, lds_off, chunk_begin, pad;
+};
+constexpr int kLFixBytes = sizeof(LFix);  // 24
+
+__device__ __forceinline__ void fcols_to_lds(const FixProgram& P, const EncCols& cols, uint8_t* lds) {
+    LFix* l = (LFix*)(lds + P.fc_lds);
+    for (int g = threadIdx.x; g < P.n_fcols; g += kBlock) {
+        const FixCol fc = P.fcols[g];
+        l[g] = LFix{cols.data[fc.col], fc.width, fc.lds_off, fc.chunk_begin, 0};
+    }
+}
 
 template <bool NTL>
 __device__ __forceinline__ void stage_tile(const FixProgram& P, const EncCols& cols, uint8_t* lds, uint64_t blob0,
                                            uint32_t rows, uint32_t T) {
     (void)T;
     const int tid = threadIdx.x;
+    (void)cols;
+    const LFix* lfc = (const LFix*)(lds + P.fc_lds);
     u32x4 v[kStageSlots];
     uint32_t dst[kStageSlots];
     bool ok[kStageSlots];
@@ -95,9 +123,9 @@ __device__ __forceinline__ void stage_tile(const FixProgram& P, const EncCols& c
         const uint8_t* base = nullptr;
         uint32_t w = 0, lo = 0, cb = 0;
         for (int g = 0; g < P.n_fcols; g++) {
-            const FixCol fc = P.fcols[g];
+            const LFix fc = lfc[g];
             const bool in = k >= (int)fc.chunk_begin;
-            base = in ? cols.data[fc.col] : base;
+            base = in ? fc.base : base;
             w = in ? fc.width : w;
             lo = in ? fc.lds_off : lo;
             cb = in ? fc.chunk_begin : cb;
@@ -108,7 +136,7 @@ __device__ __forceinline__ void stage_tile(const FixProgram& P, const EncCols& c
         dst[u] = lo + byte;
         ok[u] = byte < lim;
         if (byte + 16 <= lim) {
-            v[u] = NTL ? __builtin_nontemporal_load((const u32x4*)src) : *(const u32x4*)src;
+            v[u] = gload16<NTL>(src);
         } else if (ok[u]) {  // last, partial chunk of the final tile
             uint32_t w4[4] = {0, 0, 0, 0};
             for (uint32_t j = 0; j < lim - byte; j++) w4[j >> 2] |= (uint32_t)src[j] << (8 * (j & 3));
@@ -141,10 +169,12 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCol
     const uint64_t ntiles = (n + T - 1) / T;
     DwDesc d;
     if (s < R) d = P.dw[q];
+    fcols_to_lds(P, cols, lds);
+    __syncthreads();
     for (uint64_t tile = blockIdx.x; tile < ntiles; tile += PERSIST ? gridDim.x : ntiles) {
         const uint64_t blob0 = tile * (uint64_t)T;
         const uint32_t rows = (uint32_t)min((uint64_t)T, n - blob0);
-        if (PERSIST) __syncthreads();  // previous tile's LDS reads are done
+        if (PERSIST && tile != blockIdx.x) __syncthreads();  // previous tile's LDS reads are done
         stage_tile<NTL>(P, cols, lds, blob0, rows, (uint32_t)T);
         __syncthreads();
         if (s < R) {
@@ -187,6 +217,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw16(FixProgram P, EncC
     const uint32_t q = tid % Q4, s = tid / Q4, R = kBlock / Q4;
     DwDesc d;
     if (s < R) d = P.dw[q];
+    fcols_to_lds(P, cols, lds);
+    __syncthreads();
     stage_tile<NTL>(P, cols, lds, blob0, rows, (uint32_t)T);
     __syncthreads();
     uint32_t vals[kMaxPer];
@@ -250,6 +282,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed(FixProgram P, EncCols c
     const uint32_t nsegs = P.seg_index[B];
     for (uint32_t k = tid; k <= B; k += kBlock) s_index[k] = P.seg_index[k];
     for (uint32_t k = tid; k < nsegs; k += kBlock) s_segs[k] = P.segs[k];
+    fcols_to_lds(P, cols, lds);
+    __syncthreads();
     stage_tile<false>(P, cols, lds, blob0, rows, (uint32_t)T);
     __syncthreads();
 
@@ -957,30 +991,36 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
             if (variant == 0) variant = dw_ok ? kDefaultFixedVariant : 8;
             if ((variant >= 5 && variant <= 7 && !dw16_ok) || ((variant <= 4 || variant >= 9) && !dw_ok)) variant = 8;
             const dim3 g((unsigned)tiles), b(kBlock);
-            const size_t lds_dw = (size_t)s->fix_lds;
-            const size_t lds_dw16 = std::max<size_t>((size_t)s->fix_lds, (size_t)s->fix_T * B);
+            const size_t fcb = ((s->fcols.size() * kLFixBytes) + 15) / 16 * 16;
+            // each kernel gets the column table copied right after the LDS it uses
+            FixProgram pdw = t->fix, pdw16 = t->fix, pgen = t->fix;
+            pdw.fc_lds = s->fix_lds;
+            pdw16.fc_lds = (int32_t)std::max<size_t>((size_t)s->fix_lds, (size_t)s->fix_T * B);
+            const size_t gen_tables = (size_t)s->fix_lds + ((B + 1) * 4 + 15) / 16 * 16 + s->fsegs.size() * sizeof(FixSeg);
+            pgen.fc_lds = (int32_t)gen_tables;
+            const size_t lds_dw = (size_t)pdw.fc_lds + fcb;
+            const size_t lds_dw16 = (size_t)pdw16.fc_lds + fcb;
             switch (variant) {
-                case 1: hipLaunchKernelGGL((k_encode_fixed_dw<false, false>), g, b, lds_dw, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
-                case 2: hipLaunchKernelGGL((k_encode_fixed_dw<false, true>), g, b, lds_dw, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
-                case 3: hipLaunchKernelGGL((k_encode_fixed_dw<true, false>), g, b, lds_dw, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
-                case 4: hipLaunchKernelGGL((k_encode_fixed_dw<true, true>), g, b, lds_dw, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
-                case 5: hipLaunchKernelGGL((k_encode_fixed_dw16<false, false>), g, b, lds_dw16, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
-                case 6: hipLaunchKernelGGL((k_encode_fixed_dw16<false, true>), g, b, lds_dw16, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
-                case 7: hipLaunchKernelGGL((k_encode_fixed_dw16<true, true>), g, b, lds_dw16, st, t->fix, ec, out, (uint64_t)n, status, stv); break;
+                case 1: hipLaunchKernelGGL((k_encode_fixed_dw<false, false>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
+                case 2: hipLaunchKernelGGL((k_encode_fixed_dw<false, true>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
+                case 3: hipLaunchKernelGGL((k_encode_fixed_dw<true, false>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
+                case 4: hipLaunchKernelGGL((k_encode_fixed_dw<true, true>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
+                case 5: hipLaunchKernelGGL((k_encode_fixed_dw16<false, false>), g, b, lds_dw16, st, pdw16, ec, out, (uint64_t)n, status, stv); break;
+                case 6: hipLaunchKernelGGL((k_encode_fixed_dw16<false, true>), g, b, lds_dw16, st, pdw16, ec, out, (uint64_t)n, status, stv); break;
+                case 7: hipLaunchKernelGGL((k_encode_fixed_dw16<true, true>), g, b, lds_dw16, st, pdw16, ec, out, (uint64_t)n, status, stv); break;
                 case 9: case 10: {
                     const dim3 gp((unsigned)std::min<uint64_t>(tiles, (uint64_t)cu_count(dev) * 8));
                     if (variant == 9)
-                        hipLaunchKernelGGL((k_encode_fixed_dw<false, true, true>), gp, b, lds_dw, st, t->fix, ec, out, (uint64_t)n, status, stv);
+                        hipLaunchKernelGGL((k_encode_fixed_dw<false, true, true>), gp, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv);
                     else
-                        hipLaunchKernelGGL((k_encode_fixed_dw<true, true, true>), gp, b, lds_dw, st, t->fix, ec, out, (uint64_t)n, status, stv);
+                        hipLaunchKernelGGL((k_encode_fixed_dw<true, true, true>), gp, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv);
                     break;
                 }
                 default: variant = 8; break;
             }
             if (variant == 8) {
-                const size_t lds = (size_t)s->fix_lds + ((B + 1) * 4 + 15) / 16 * 16 + s->fsegs.size() * sizeof(FixSeg);
-                hipLaunchKernelGGL(k_encode_fixed, dim3((unsigned)tiles), dim3(kBlock), lds, st, t->fix, ec, out,
-                                   (uint64_t)n, status, stv);
+                hipLaunchKernelGGL(k_encode_fixed, dim3((unsigned)tiles), dim3(kBlock), gen_tables + fcb, st, pgen, ec,
+                                   out, (uint64_t)n, status, stv);
             }
             HIP_TRY(hipGetLastError());
             return PACKOS_OK;

@@ -100,6 +100,7 @@ struct FixProgram {
     const FixCol* fcols;
     const DwDesc* dw;            // B/4 entries when B % 4 == 0
     int32_t B, T, n_fcols, lds_bytes, total_chunks, overflow;
+    int32_t fc_lds;              // LDS offset of the per-launch copy of fcols (set at launch)
 };
 
 // ---------------------------------------------------------------- decode ----
