@@ -47,7 +47,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // fixed-layout encode variant used when the caller does not pick one
 // (1..4: dword stores, 5..7: LDS re-staged 16-B stores; NT = non-temporal)
-constexpr int kDefaultFixedVariant = 1;
+constexpr int kDefaultFixedVariant = 2;
 
 __device__ __forceinline__ uint16_t enc_header(int64_t off, int tag) {
     return (uint16_t)((((uint64_t)off) << 3) & 0xFFFFu) | (uint16_t)(tag & 7);
@@ -157,7 +157,7 @@ __device__ __forceinline__ uint32_t lds_dword_at(const uint32_t* l32, uint32_t a
 // of blobs s, s+R, s+2R ... of the tile; its byte sources sit in registers.
 // PERSIST: a grid of ~CUs x 8 workgroups walks the tiles (descriptors loaded
 // once per workgroup instead of once per tile).
-template <bool NTL, bool NTS, bool PERSIST = false>
+template <bool NTL, bool NTS, bool PERSIST = false, int U = 1>
 __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCols cols, uint8_t* __restrict__ out,
                                                             uint64_t n, uint32_t* __restrict__ status,
                                                             uint32_t st_val) {
@@ -180,18 +180,30 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCol
         if (s < R) {
             const uint32_t* l32 = (const uint32_t*)lds;
             uint32_t* o32 = (uint32_t*)(out + blob0 * (uint64_t)P.B) + q;
-            for (uint32_t j = s; j < rows; j += R) {
-                uint32_t v = d.cval;
+            // U blobs per iteration: their LDS reads issue back to back
+            for (uint32_t j = s; j < rows; j += U * R) {
+                uint32_t v[U];
 #pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    if ((uint32_t)g < d.nseg) {
-                        uint32_t x = lds_dword_at(l32, (uint32_t)d.seg[g].a + j * d.seg[g].w) & d.seg[g].mask;
-                        if (d.seg[g].flags & 1u) x = x ? (d.seg[g].mask & 0x01010101u) : 0u;
-                        v |= x;
+                for (int uu = 0; uu < U; uu++) {
+                    const uint32_t jj = j + uu * R;
+                    v[uu] = d.cval;
+#pragma unroll
+                    for (int g = 0; g < 4; g++) {
+                        if ((uint32_t)g < d.nseg) {
+                            uint32_t x = lds_dword_at(l32, (uint32_t)d.seg[g].a + jj * d.seg[g].w) & d.seg[g].mask;
+                            if (d.seg[g].flags & 1u) x = x ? (d.seg[g].mask & 0x01010101u) : 0u;
+                            v[uu] |= x;
+                        }
                     }
                 }
-                if (NTS) __builtin_nontemporal_store(v, o32 + (uint64_t)j * Q4);
-                else o32[(uint64_t)j * Q4] = v;
+#pragma unroll
+                for (int uu = 0; uu < U; uu++) {
+                    const uint32_t jj = j + uu * R;
+                    if (jj < rows) {
+                        if (NTS) __builtin_nontemporal_store(v[uu], o32 + (uint64_t)jj * Q4);
+                        else o32[(uint64_t)jj * Q4] = v[uu];
+                    }
+                }
             }
         }
         if (status)
@@ -1016,6 +1028,9 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
                         hipLaunchKernelGGL((k_encode_fixed_dw<true, true, true>), gp, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv);
                     break;
                 }
+                case 11: hipLaunchKernelGGL((k_encode_fixed_dw<false, true, false, 2>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
+                case 12: hipLaunchKernelGGL((k_encode_fixed_dw<true, true, false, 2>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
+                case 13: hipLaunchKernelGGL((k_encode_fixed_dw<false, true, false, 4>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
                 default: variant = 8; break;
             }
             if (variant == 8) {
