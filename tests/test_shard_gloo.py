@@ -1,0 +1,81 @@
+"""N>1 path on CPU: byte-balanced shards, no data-path collective, world size 2
+over gloo.  Each rank encodes only its shard (the CPU oracle stands in for the
+device encode here — there is no GPU in this test); rank 0 stitches the
+per-shard arenas/offsets and must reproduce the single-shot encoding
+bit-for-bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle_bridge as ob
+from packos_amd.api import CompiledSchema
+from packos_amd.configs import CONFIGS, make_columns
+from packos_amd.shard import blob_sizes_host, plan_shards, slice_columns, stitch_offsets
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cfg_name, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = CONFIGS[cfg_name]
+    hc = make_columns(cfg, n=n)
+    schema = CompiledSchema(cfg.chain, cfg.mode)
+    sizes = blob_sizes_host(schema, hc)
+    shards = plan_shards(sizes, world)
+    lo, hi = shards[rank]
+    mine = slice_columns(hc, lo, hi)
+    arena, offs, st = ob.encode(cfg.chain, mine, cfg.mode)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, (lo, hi, arena.tobytes(), offs.tolist()))
+    if rank == 0:
+        full_arena, full_offs, _ = ob.encode(cfg.chain, hc, cfg.mode)
+        stitched = b"".join(g[2] for g in gathered)
+        offsets = stitch_offsets([np.asarray(g[3], np.uint64) for g in gathered])
+        bytes_per = [len(g[2]) for g in gathered]
+        q.put((stitched == full_arena.tobytes(), np.array_equal(offsets, full_offs),
+               [(g[0], g[1]) for g in gathered], bytes_per, np.array_equal(sizes, np.diff(full_offs.astype(np.int64)))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg_name,n", [("C5", 3000), ("C3", 4000), ("M", 2048)])
+def test_two_rank_shards_stitch(cfg_name, n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, cfg_name, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    same_bytes, same_offs, ranges, bytes_per, sizes_ok = res
+    assert sizes_ok, "host size planning disagrees with the encoder"
+    assert same_bytes and same_offs
+    assert ranges[0][0] == 0 and ranges[0][1] == ranges[1][0] and ranges[1][1] == n
+    # byte-balanced: the two shards differ by at most one blob's worth (+slack)
+    assert abs(bytes_per[0] - bytes_per[1]) <= 4200
+
+
+def test_plan_shards_properties():
+    rng = np.random.default_rng(0)
+    sizes = rng.integers(64, 4096, 10_000)
+    for world in (1, 2, 3, 8):
+        sh = plan_shards(sizes, world)
+        assert len(sh) == world and sh[0][0] == 0 and sh[-1][1] == len(sizes)
+        assert all(a[1] == b[0] for a, b in zip(sh, sh[1:]))
+        tot = [int(sizes[lo:hi].sum()) for lo, hi in sh]
+        assert max(tot) - min(tot) <= 2 * 4096
+    assert plan_shards(np.zeros(0, np.int64), 4) == [(0, 0)] * 4
