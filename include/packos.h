@@ -162,6 +162,11 @@ int  packos_schema_column_info(const packos_schema* s, int col, packos_column_in
 /* Blob size in bytes when the schema has no variable-width leaf and a call
  * passes no validity columns (every nullable present), else -1.              */
 int64_t packos_schema_fixed_blob_size(const packos_schema* s);
+/* 1 when packos_decode_batch can use the tiled fixed-layout decoder for this
+ * schema (fixed size B, B % 4 == 0, B <= 1024, and the all-present blob
+ * decodes cleanly), else 0.  Decided at compile time, without a GPU; results
+ * never depend on it (non-canonical blobs fall back to the exact decoder).  */
+int  packos_schema_decode_fast(const packos_schema* s);
 /* Host-side dump of the compiled layout program (debug/testing). Returns the
  * number of bytes needed (including NUL); writes at most cap bytes.          */
 size_t packos_schema_describe(const packos_schema* s, char* buf, size_t cap);

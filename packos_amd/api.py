@@ -83,6 +83,11 @@ class CompiledSchema:
     def fixed_blob_size(self) -> int:
         return int(lib().packos_schema_fixed_blob_size(self._h))
 
+    @property
+    def decode_fast(self) -> bool:
+        """True when decode_batch uses the tiled fixed-layout decoder."""
+        return bool(lib().packos_schema_decode_fast(self._h))
+
     def all_present_size(self) -> int:
         return int(lib().packos_schema_blob_size_host(self._h, None, None))
 
@@ -255,13 +260,20 @@ class DecodedColumns:
 
 
 def decode_batch(schema: CompiledSchema, arena, offsets=None, n: Optional[int] = None, stride: int = 0,
-                 stream=None):
-    """schema.DecodeBuffer over every blob; returns (DecodedColumns, status)."""
+                 stream=None, out: Optional[DecodedColumns] = None, status=None):
+    """schema.DecodeBuffer over every blob; returns (DecodedColumns, status).
+    `out` / `status` reuse buffers from an earlier call (no allocation)."""
     torch = _torch()
     if n is None:
         n = offsets.numel() - 1
-    out = DecodedColumns(schema, n, arena.device)
-    status = torch.empty(max(n, 1), dtype=torch.int32, device=arena.device)
+    if out is None:
+        out = DecodedColumns(schema, n, arena.device)
+    elif out.n < n or out.schema is not schema:
+        raise ValueError("decode_batch: `out` was allocated for another schema or a smaller batch")
+    if status is None:
+        status = torch.empty(max(n, 1), dtype=torch.int32, device=arena.device)
+    elif status.numel() < n or status.dtype != torch.int32:
+        raise ValueError("decode_batch: `status` needs n int32 entries")
     check(lib().packos_decode_batch(schema.handle, arena.data_ptr(),
                                     None if offsets is None else offsets.data_ptr(), stride, n,
                                     out.ctypes_array(), status.data_ptr(), _stream_ptr(stream)),

@@ -385,6 +385,38 @@ struct Builder {
         }
         s->fix_lds = (int)lds + 16;
         s->fix_chunks = (int)chunks;
+        // decode fast path tables: per-dword constant check, per-column
+        // blob offset, canonical blob (payload bytes zero)
+        s->dchk.clear();
+        s->canon.assign((size_t)B, 0);
+        for (int64_t q = 0; q < (B + 3) / 4; q++) {
+            uint32_t cm = 0, cv = 0;
+            for (int b = 0; b < 4; b++)
+                if (4 * q + b < B && bm[4 * q + b].col < 0) {
+                    cm |= 0xFFu << (8 * b);
+                    cv |= (uint32_t)bm[4 * q + b].val << (8 * b);
+                    s->canon[4 * q + b] = bm[4 * q + b].val;
+                }
+            s->dchk.push_back(cm);
+            s->dchk.push_back(cv);
+        }
+        s->dfix.clear();
+        uint32_t units = 0;
+        for (const FixCol& fc : s->fcols) {
+            DecFix df{};
+            df.col = fc.col;
+            df.width = fc.width;
+            df.blob_off = UINT32_MAX;
+            for (int64_t q = 0; q < B; q++)
+                if (bm[q].col == fc.col && bm[q].off == 0) { df.blob_off = (uint32_t)q; break; }
+            if (df.blob_off == UINT32_MAX) fail(PACKOS_E_SCHEMA, "internal: fixed column not in layout");
+            df.flags = bm[df.blob_off].is_bool ? 1u : 0u;
+            df.magic = fc.width > 1 ? (uint32_t)(((1ull << 32) + fc.width - 1) / fc.width) : 0u;
+            df.unit_begin = units;
+            units += (uint32_t)T * fc.width / 16;
+            s->dfix.push_back(df);
+        }
+        s->dfix_units = (int)units;
         if (s->fix_lds > 60 * 1024) return;
         // segments for each dword r of a 4-blob period
         s->fsegs.clear();
@@ -609,6 +641,7 @@ int packos_schema_compile(const char* schema_json, int mode, packos_schema** out
         b.build_encode();
         b.build_fixed();
         b.build_decode();
+        s->dec_fast = canonical_decodes(s) ? 1 : 0;
         b.build_info();
         b.build_describe();
     } catch (const CompileError& e) {
@@ -632,6 +665,8 @@ int packos_schema_column_info(const packos_schema* s, int col, packos_column_inf
     *out = s->col_info[col];
     return PACKOS_OK;
 }
+
+int packos_schema_decode_fast(const packos_schema* s) { return s && s->dec_fast == 1 ? 1 : 0; }
 
 int64_t packos_schema_fixed_blob_size(const packos_schema* s) {
     if (!s || s->has_var) return -1;

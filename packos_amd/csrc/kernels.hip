@@ -580,10 +580,10 @@ struct DSeq {
     int next_type, cur_type;
 };
 
-__device__ __forceinline__ uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+__host__ __device__ __forceinline__ uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
 
 // NewSeqGetAccess (seqget.go:22-47)
-__device__ __forceinline__ int dseq_init(DSeq& s, const uint8_t* a, uint64_t start, int64_t len) {
+__host__ __device__ __forceinline__ int dseq_init(DSeq& s, const uint8_t* a, uint64_t start, int64_t len) {
     if (len < 4) return 1;
     const uint16_t h0 = rd16(a + start);
     const int64_t base = h0 >> 3;
@@ -595,7 +595,7 @@ __device__ __forceinline__ int dseq_init(DSeq& s, const uint8_t* a, uint64_t sta
     return 0;
 }
 // Advance (seqget.go:85-103): 0 ok, 1 out of bounds, 2 Go panic (unchecked header read)
-__device__ __forceinline__ int dseq_advance(DSeq& s, const uint8_t* a) {
+__host__ __device__ __forceinline__ int dseq_advance(DSeq& s, const uint8_t* a) {
     if (s.pos + 2 > s.count) return 1;
     s.pos++;
     s.cur_off = s.next_off;
@@ -609,7 +609,7 @@ __device__ __forceinline__ int dseq_advance(DSeq& s, const uint8_t* a) {
     return 0;
 }
 // precheck (schema.go:997-1013): 0 ok else ErrConstraintViolated
-__device__ __forceinline__ int dprecheck(const DSeq& s, int tag, int64_t hint, bool nullable, int64_t& w) {
+__host__ __device__ __forceinline__ int dprecheck(const DSeq& s, int tag, int64_t hint, bool nullable, int64_t& w) {
     if (s.pos >= s.count) return 3;
     if (s.next_off > s.len) return 3;
     if (s.cur_type != tag) return 3;
@@ -626,19 +626,16 @@ struct Frame {
     int k;
 };
 
-__global__ __launch_bounds__(kBlock) void k_decode(DecProgram P, DecCols cols, const uint8_t* __restrict__ arena,
-                                                   const uint64_t* __restrict__ offs, uint64_t stride, uint64_t n,
-                                                   uint32_t* __restrict__ status) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t a0 = offs ? offs[i] : i * stride;
-    const uint64_t a1 = offs ? offs[i + 1] : (i + 1) * stride;
+// DecodeBuffer (schema.go:893-910) for blob i = arena[a0, a1): writes its
+// leaves into the output columns and returns the packed status word.  Host +
+// device: the host runs it once on the canonical blob to qualify a schema for
+// the fixed-layout fast path (same code, so the qualification is exact).
+__host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& cols, const uint8_t* arena, uint64_t a0,
+                                         uint64_t a1, uint64_t i) {
     Frame st[kDecDepth];
     int d = 0;
-    if (dseq_init(st[0].q, arena, a0, (int64_t)(a1 - a0))) {
-        status[i] = (uint32_t)PACKOS_ERR_INVALID_FORMAT;  // position -1
-        return;
-    }
+    if (dseq_init(st[0].q, arena, a0, (int64_t)(a1 - a0)))
+        return (uint32_t)PACKOS_ERR_INVALID_FORMAT;  // position -1
     st[0].node = P.root;
     st[0].k = 0;
     int err = 0;
@@ -736,7 +733,153 @@ __global__ __launch_bounds__(kBlock) void k_decode(DecProgram P, DecCols cols, c
         if (err == kPanic) sv = PACKOS_STATUS_PANIC | posv;
         else sv = (uint32_t)(d == 0 ? err : PACKOS_ERR_INVALID_FORMAT) | posv;
     }
-    status[i] = sv;
+    return sv;
+}
+
+// generic decode: one thread per blob
+__global__ __launch_bounds__(kBlock) void k_decode(DecProgram P, DecCols cols, const uint8_t* __restrict__ arena,
+                                                   const uint64_t* __restrict__ offs, uint64_t stride, uint64_t n,
+                                                   uint32_t* __restrict__ status) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t a0 = offs ? offs[i] : i * stride;
+    const uint64_t a1 = offs ? offs[i + 1] : (i + 1) * stride;
+    status[i] = decode_blob(P, cols, arena, a0, a1, i);
+}
+
+// Fixed-layout decode (the transpose of k_encode_fixed_dw).  A workgroup
+// takes a tile of T consecutive blobs, which must lie back to back in the
+// arena (size B each, 16-B aligned start; otherwise the whole tile goes to
+// decode_blob):
+//   1. stage the tile's T*B bytes in LDS with 16-B loads;
+//   2. compare every blob dword's constant bytes (header words, literals,
+//      map keys) with the canonical layout -> per-blob fail flag;
+//   3. write every fixed column's T rows as 16-B output units gathered from
+//      the staged blobs (funnel-shifted dword reads; bools normalised);
+//   4. mark validity, then run decode_blob for the (rare) blobs that failed
+//      the check, overwriting their rows with the exact reference behaviour.
+struct LDec {                 // LDS copy of a DecFix with its output column resolved
+    uint8_t* dst;
+    uint32_t width, blob_off, flags, magic, unit_begin, pad;
+};
+
+__device__ __forceinline__ uint32_t lds_u8(const uint32_t* lds, uint32_t a) { return (lds[a >> 2] >> (8 * (a & 3))) & 0xFFu; }
+
+__global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecProgram P, DecCols cols,
+                                                         const uint8_t* __restrict__ arena,
+                                                         const uint64_t* __restrict__ offs, uint64_t n,
+                                                         uint32_t* __restrict__ status) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
+    uint32_t* lds = (uint32_t*)lds_raw;
+    const uint32_t B = (uint32_t)F.B, T = (uint32_t)F.T, QW = (B + 3) >> 2;
+    const uint64_t blob0 = (uint64_t)blockIdx.x * T;
+    const uint32_t rows = (uint32_t)min((uint64_t)T, n - blob0);
+    const int tid = threadIdx.x;
+    uint32_t* chk = lds + (T * B / 4 + 4);
+    uint32_t* fail = chk + 2 * QW;
+    LDec* ltab = (LDec*)(fail + ((T + 1) & ~1u));
+
+    uint64_t base = blob0 * B;
+    bool ok = true;
+    if (offs) {
+        base = offs[blob0];
+        for (uint32_t j = tid; j <= rows; j += kBlock) ok &= offs[blob0 + j] == base + (uint64_t)j * B;
+        ok &= (base & 15) == 0;
+    }
+    for (uint32_t q = tid; q < 2 * QW; q += kBlock) chk[q] = F.chk[q];
+    for (uint32_t j = tid; j < rows; j += kBlock) fail[j] = 0;
+    for (int c = tid; c < F.n_cols; c += kBlock) {
+        const DecFix fc = F.cols[c];
+        ltab[c] = LDec{cols.data[fc.col], fc.width, fc.blob_off, fc.flags, fc.magic, fc.unit_begin, 0};
+    }
+    if (!__syncthreads_and(ok)) {
+        for (uint32_t j = tid; j < rows; j += kBlock) {
+            const uint64_t i = blob0 + j;
+            status[i] = decode_blob(P, cols, arena, offs[i], offs[i + 1], i);
+        }
+        return;
+    }
+    // 1. stage
+    const uint32_t bytes = rows * B;
+    {
+        const g_u32x4* src = (const g_u32x4*)(arena + base);
+        const uint32_t n16 = bytes >> 4;
+        for (uint32_t k = tid; k < n16; k += kBlock) ((u32x4*)lds)[k] = __builtin_nontemporal_load(src + k);
+        const uint8_t* src1 = arena + base;
+        for (uint32_t k = n16 * 16 + tid; k < bytes; k += kBlock) lds_raw[k] = src1[k];
+    }
+    __syncthreads();
+    // 2. constant-byte check
+    if ((B & 3) == 0) {
+        const uint32_t Q = B >> 2;
+        for (uint32_t e = tid; e < bytes / 4; e += kBlock) {
+            const uint32_t j = F.q_magic ? __umulhi(e, F.q_magic) : e;
+            const uint32_t q = e - j * Q;
+            if ((lds[e] & chk[2 * q]) != chk[2 * q + 1]) fail[j] = 1;
+        }
+    } else {
+        for (uint32_t t = tid; t < bytes; t += kBlock) {
+            const uint32_t j = __umulhi(t, F.b_magic);
+            const uint32_t p = t - j * B, sh = 8 * (p & 3);
+            const uint32_t m = (chk[2 * (p >> 2)] >> sh) & 0xFFu, v = (chk[2 * (p >> 2) + 1] >> sh) & 0xFFu;
+            if ((lds_u8(lds, t) & m) != v) fail[j] = 1;
+        }
+    }
+    // 3. columns: unit u = 16 output bytes of one column
+    for (uint32_t u = tid; u < (uint32_t)F.total_units; u += kBlock) {
+        int sel = 0;
+        for (int c = 1; c < F.n_cols; c++) sel = u >= ltab[c].unit_begin ? c : sel;
+        const LDec L = ltab[sel];
+        const uint32_t w = L.width;
+        const uint32_t t0 = (u - L.unit_begin) * 16;
+        const uint32_t R = rows * w;
+        if (t0 >= R) continue;
+        uint8_t* dst = L.dst + blob0 * w + t0;
+        if (t0 + 16 <= R) {
+            u32x4 v;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t b = t0 + 4 * k;
+                uint32_t j = w > 1 ? __umulhi(b, L.magic) : b;
+                uint32_t r = b - j * w;
+                uint32_t x;
+                if (r + 4 <= w) {
+                    const uint32_t a = j * B + L.blob_off + r;
+                    x = __builtin_amdgcn_alignbyte(lds[(a >> 2) + 1], lds[a >> 2], a & 3);
+                } else {
+                    x = 0;
+                    for (int y = 0; y < 4; y++) {
+                        x |= lds_u8(lds, j * B + L.blob_off + r) << (8 * y);
+                        if (++r == w) { r = 0; j++; }
+                    }
+                }
+                if (L.flags & 1u) {
+                    x |= x >> 4; x |= x >> 2; x |= x >> 1;
+                    x &= 0x01010101u;
+                }
+                v[k] = x;
+            }
+            *(u32x4*)dst = v;
+        } else {
+            for (uint32_t b = t0; b < R; b++) {
+                const uint32_t j = w > 1 ? __umulhi(b, L.magic) : b;
+                uint32_t x = lds_u8(lds, j * B + L.blob_off + (b - j * w));
+                if (L.flags & 1u) x = x != 0;
+                dst[b - t0] = (uint8_t)x;
+            }
+        }
+    }
+    // 4. validity (every node is present in the canonical layout)
+    for (int c = 0; c < F.n_all_cols; c++)
+        if (cols.valid[c])
+            for (uint32_t j = tid; j < rows; j += kBlock) cols.valid[c][blob0 + j] = 1;
+    __syncthreads();
+    for (uint32_t j = tid; j < rows; j += kBlock) {
+        const uint64_t i = blob0 + j;
+        uint32_t sv = 0;
+        if (fail[j]) sv = decode_blob(P, cols, arena, offs ? offs[i] : i * B, offs ? offs[i + 1] : (i + 1) * B, i);
+        status[i] = sv;
+    }
 }
 
 // =========================================================================
@@ -828,6 +971,35 @@ int cu_count(int dev) {
     return cache[dev];
 }
 
+// Does the all-present blob of a fixed schema decode cleanly?  Runs the same
+// decode_blob the device runs, on the host, over the canonical blob (zero
+// payload bytes).  Only then may k_decode_fixed treat "constant bytes match"
+// as "decodes like the canonical blob".
+}  // namespace
+
+bool packos::canonical_decodes(const packos_schema* s) {
+    if (s->has_var || s->canon.empty() || s->fix_T <= 0) return false;
+    int maxd = 0;
+    for (const Node& nd : s->nodes) maxd = std::max(maxd, nd.depth);
+    if (maxd >= kDecDepth) return false;
+    const size_t nc = s->col_node.size();
+    std::vector<uint8_t> data(nc * 1024 + 16, 0), valid(nc, 0);
+    std::vector<uint64_t> start(nc, 0);
+    std::vector<uint32_t> length(nc, 0);
+    DecCols dc;
+    memset(&dc, 0, sizeof(dc));
+    for (size_t c = 0; c < nc; c++) {
+        dc.data[c] = data.data() + c * 1024;
+        dc.valid[c] = &valid[c];
+        dc.start[c] = &start[c];
+        dc.length[c] = &length[c];
+    }
+    DecProgram P{s->dnodes.data(), s->dkids.data(), s->lits.data(), 0};
+    return decode_blob(P, dc, s->canon.data(), 0, s->canon.size(), 0) == 0;
+}
+
+namespace {
+
 int fill_enc_cols(const packos_schema* s, const packos_column* cols, EncCols& ec, bool* any_nil) {
     memset(&ec, 0, sizeof(ec));
     *any_nil = false;
@@ -873,6 +1045,8 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     size_t o_fdw = put_bytes(blob, s->fdw);
     size_t o_dnodes = put_bytes(blob, s->dnodes);
     size_t o_dkids = put_bytes(blob, s->dkids);
+    size_t o_dfix = put_bytes(blob, s->dfix);
+    size_t o_dchk = put_bytes(blob, s->dchk);
     DeviceTables t;
     t.device = device;
     HIP_TRY(hipMalloc(&t.block, blob.size()));
@@ -900,6 +1074,19 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     t.dec.kids = (const int32_t*)(b + o_dkids);
     t.dec.lits = b + o_lits;
     t.dec.root = 0;
+    t.dfix.cols = (const DecFix*)(b + o_dfix);
+    t.dfix.chk = (const uint32_t*)(b + o_dchk);
+    t.dfix.B = (int)s->all_present_size;
+    t.dfix.T = s->fix_T;
+    t.dfix.n_cols = (int)s->dfix.size();
+    t.dfix.total_units = s->dfix_units;
+    {
+        const uint64_t q = (uint64_t)std::max<int64_t>(1, s->all_present_size / 4);
+        const uint64_t bb = (uint64_t)std::max<int64_t>(2, s->all_present_size);
+        t.dfix.q_magic = q > 1 ? (uint32_t)(((1ull << 32) + q - 1) / q) : 0u;
+        t.dfix.b_magic = (uint32_t)(((1ull << 32) + bb - 1) / bb);
+    }
+    t.dfix.n_all_cols = (int)s->col_node.size();
     s->dev.push_back(t);
     *out = &s->dev.back();
     return PACKOS_OK;
@@ -1095,8 +1282,19 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
         if (!(scalar && nd.nullable) && nd.kind != K_TUPLE && nd.kind != K_MAP) dc.valid[c] = nullptr;
     }
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_decode, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, t->dec, dc, arena,
-                       offsets, stride, (uint64_t)n, status);
+    const int64_t B = s->all_present_size;
+    bool fast = s->dec_fast == 1 && ((uintptr_t)arena & 15) == 0 && (offsets || stride == (uint64_t)B) &&
+                !getenv("PACKOS_DECODE_GENERIC");
+    for (const DecFix& f : s->dfix) fast = fast && ((uintptr_t)dc.data[f.col] & 15) == 0;
+    if (fast) {
+        const uint32_t T = (uint32_t)s->fix_T, QW = (uint32_t)((B + 3) / 4);
+        const size_t lds = (size_t)T * B + 16 + 8 * QW + 4 * ((T + 1) & ~1u) + 32 * s->dfix.size();
+        hipLaunchKernelGGL(k_decode_fixed, dim3((unsigned)((n + T - 1) / T)), dim3(kBlock), lds, st, t->dfix, t->dec,
+                           dc, arena, offsets, (uint64_t)n, status);
+    } else {
+        hipLaunchKernelGGL(k_decode, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, t->dec, dc,
+                           arena, offsets, stride, (uint64_t)n, status);
+    }
     HIP_TRY(hipGetLastError());
     return PACKOS_OK;
 }

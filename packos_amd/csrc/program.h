@@ -124,6 +124,29 @@ struct DecProgram {
     int32_t root;
 };
 
+// Fixed-layout decode fast path.  A blob whose length is B and whose
+// constant bytes (header words, MATCH literals, map keys) equal those of the
+// schema's all-present layout walks the SeqGetAccess machine exactly like the
+// canonical blob does, so its leaves sit at compile-time positions.
+struct DecFix {
+    int32_t col;
+    uint32_t width;
+    uint32_t blob_off;     // first payload byte of the leaf inside the blob
+    uint32_t flags;        // bit0: bool (normalise to 0/1)
+    uint32_t magic;        // ceil(2^32 / width) for width > 1 (division by width)
+    uint32_t unit_begin;   // first 16-B output unit of this column in a full tile
+    uint32_t pad[2];
+};
+
+struct DecFixProgram {
+    const DecFix* cols;
+    const uint32_t* chk;   // ceil(B/4) pairs {constant-byte mask, constant value}
+    int32_t B, T, n_cols, total_units;
+    uint32_t q_magic;      // B % 4 == 0: ceil(2^32 / (B/4)) (0 when B/4 == 1)
+    uint32_t b_magic;      // B % 4 != 0: ceil(2^32 / B)
+    int32_t n_all_cols;    // every schema column (validity marking)
+};
+
 // column pointer tables passed by value as kernel arguments
 struct EncCols {
     const uint8_t* data[kMaxCols];

@@ -30,6 +30,7 @@ struct DeviceTables {
     EncProgram enc{};
     FixProgram fix{};
     DecProgram dec{};
+    DecFixProgram dfix{};
 };
 
 }  // namespace packos
@@ -62,6 +63,13 @@ struct packos_schema {
     // decode program
     std::vector<packos::DecNode> dnodes;
     std::vector<int32_t> dkids;
+    // fixed-layout decode fast path (B % 4 == 0, B <= 1024); dec_fast is set
+    // when the canonical blob decodes cleanly (checked on first upload)
+    std::vector<packos::DecFix> dfix;
+    std::vector<uint32_t> dchk;
+    std::vector<uint8_t> canon;       // all-present blob, zero payload bytes
+    int dfix_units = 0;
+    int dec_fast = 0;                 // 1: canonical blob decodes (set at compile)
 
     std::string describe;
 
@@ -73,4 +81,6 @@ namespace packos {
 // thread-local last error string
 void set_error(const std::string& m);
 int upload_tables(packos_schema* s, int device, DeviceTables** out);
+// host run of the device decoder over the canonical blob (kernels.hip)
+bool canonical_decodes(const packos_schema* s);
 }  // namespace packos

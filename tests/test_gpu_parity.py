@@ -121,23 +121,28 @@ def test_empty_batch_and_empty_chain():
 
 
 # --------------------------------------------------------------- decode ----
-def gpu_decode(chain, arena_np, offs_np, n):
+def gpu_decode(chain, arena_np, offs_np, n, stride=0):
     T = torch()
     s = CompiledSchema(chain, 0)
     arena = T.from_numpy(arena_np if arena_np.size else np.zeros(16, np.uint8)).to("cuda:0")
-    offs = T.from_numpy(offs_np.astype(np.int64)).to("cuda:0")
-    out, st = decode_batch(s, arena, offs, n)
+    offs = None if stride else T.from_numpy(offs_np.astype(np.int64)).to("cuda:0")
+    out, st = decode_batch(s, arena, offs, n, stride=stride)
     T.cuda.synchronize()
     return out, st.cpu().numpy().astype(np.uint32)
 
 
-def assert_same_decode(chain, arena, offs, n, what=""):
+def assert_same_decode(chain, arena, offs, n, what="", stride=0):
+    """Statuses must match for every blob; leaf columns for every blob that
+    decodes (status 0).  DecodeBuffer returns (nil, err) on failure
+    (schema/schema.go:900-903), so a failing blob's columns are unspecified
+    (the fixed-layout fast path may leave tile data in them)."""
     o_out, o_st = ob.decode(chain, arena, offs, n, nthreads=8)
-    g_out, g_st = gpu_decode(chain, arena, offs, n)
+    g_out, g_st = gpu_decode(chain, arena, offs, n, stride)
     if not np.array_equal(o_st, g_st):
         bad = int(np.nonzero(o_st != g_st)[0][0])
         raise AssertionError(f"{what}: status blob {bad}: oracle {o_st[bad]:#x} gpu {g_st[bad]:#x}")
-    for c in range(len(o_out.specs)):
+    ok = o_st[:n] == 0
+    for c, sp in enumerate(o_out.specs):
         for name in ("data", "valid", "start", "length"):
             a = getattr(o_out, name)[c]
             b = getattr(g_out, name)[c]
@@ -148,7 +153,13 @@ def assert_same_decode(chain, arena, offs, n, what=""):
                 bn = bn.astype(np.uint64)
             if name == "length":
                 bn = bn.astype(np.uint32)
-            assert np.array_equal(a[: bn.size], bn[: a.size]), f"{what}: column {c} {name}"
+            if name == "data":
+                w = sp.width
+                a2, b2 = a[: n * w].reshape(n, w), bn[: n * w].reshape(n, w)
+                same = np.array_equal(a2[ok], b2[ok])
+            else:
+                same = np.array_equal(a[:n][ok], bn[:n][ok])
+            assert same, f"{what}: column {c} {name}"
     return g_st
 
 
@@ -213,6 +224,51 @@ def test_random_decode_corrupted(seed):
         noffs.append(noffs[-1] + int(ends_cut[i] - starts[i]))
     arena2 = np.concatenate(pieces) if pieces else np.zeros(0, np.uint8)
     assert_same_decode(chain, arena2, np.asarray(noffs, np.uint64), n, f"corrupt seed {seed}")
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_fixed_decode_fast_path(seed):
+    """Fixed-size schemas take the tiled fast path (k_decode_fixed).  In-place
+    corruption keeps the tiles contiguous, so corrupted blobs go through the
+    constant-byte check and fall back to decode_blob inside the same tile.
+    Covers offsets and stride addressing and ragged last tiles."""
+    rng = np.random.default_rng(1000 + seed)
+    chain = rand_chain(seed, allow_var=False, allow_null=False)
+    s = CompiledSchema(chain, 0)
+    B = s.fixed_blob_size
+    if B <= 0:
+        pytest.skip("schema has no fixed layout")
+    n = int(rng.integers(1, 3000))
+    hc = HostColumns.from_rows(chain, rand_rows(chain, n, seed + 7))
+    arena, offs, _ = ob.encode(chain, hc, 0)
+    arena = arena.copy()
+    for i in np.nonzero(rng.random(n) < 0.05)[0]:
+        a, b = int(offs[i]), int(offs[i + 1])
+        if b > a:
+            arena[a + int(rng.integers(0, b - a))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    st = assert_same_decode(chain, arena, offs, n, f"fast offs seed {seed}")
+    if np.all(np.diff(offs.astype(np.int64)) == B):  # no nil containers: stride addressing
+        st2 = assert_same_decode(chain, arena, offs, n, f"fast stride seed {seed}", stride=B)
+        assert np.array_equal(st, st2)
+
+
+@pytest.mark.parametrize("name", ["M", "C2", "C4"])
+def test_fixed_decode_fast_matches_generic(name, monkeypatch):
+    """Fast path and the generic thread-per-blob kernel give identical columns."""
+    T = torch()
+    cfg = CONFIGS[name]
+    n = 5000
+    hc = make_columns(cfg, n=n)
+    arena, offs, _ = ob.encode(cfg.chain, hc, 0, nthreads=8)
+    f_out, f_st = gpu_decode(cfg.chain, arena, offs, n)
+    monkeypatch.setenv("PACKOS_DECODE_GENERIC", "1")
+    g_out, g_st = gpu_decode(cfg.chain, arena, offs, n)
+    assert (f_st == 0).all() and (g_st == 0).all()
+    for c in range(len(f_out.schema.specs)):
+        for name_ in ("data", "valid"):
+            a, b = getattr(f_out, name_)[c], getattr(g_out, name_)[c]
+            if a is not None:
+                assert T.equal(a, b), f"{name} column {c} {name_}"
 
 
 @pytest.mark.parametrize("name,n", [("C3", 30_000), ("C4", 30_000), ("M", 30_000), ("C5", 5000)])

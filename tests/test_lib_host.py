@@ -52,6 +52,30 @@ def test_config_blob_sizes():
     assert CompiledSchema(CONFIGS["C5"].chain).fixed_blob_size == -1
 
 
+def test_decode_fast_eligibility_configs():
+    fast = {k: CompiledSchema(c.chain, c.mode).decode_fast for k, c in CONFIGS.items()}
+    assert fast == {"M": True, "C1": True, "C2": True, "C3": False, "C4": True, "C5": False}
+    from packos_amd.schema import SChain, STuple, SInt32
+    # a present empty tuple is written as 10 00, which DecodeBuffer rejects
+    assert not CompiledSchema(SChain(SInt32, STuple())).decode_fast
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_decode_fast_eligibility_vs_oracle(seed):
+    """The compiler qualifies a fixed schema for the tiled decoder by running
+    the (host-compiled) device decoder on the canonical blob; that must agree
+    with the oracle's DecodeBuffer on an all-present blob of the schema."""
+    chain = rand_chain(seed, allow_var=False)
+    s = CompiledSchema(chain, 0)
+    B = s.fixed_blob_size
+    hc = HostColumns.from_rows(chain, rand_rows(chain, 1, seed, nil_p=0.0))
+    arena, offs, _ = ob.encode(chain, hc, 0)
+    _, st = ob.decode(chain, arena, offs, 1)
+    depth = max((d for _, d, *_ in chain.walk()), default=0)
+    expect = 0 < B <= 1024 and int(st[0]) == 0 and depth < 7
+    assert s.decode_fast == expect, (B, hex(int(st[0])), depth)
+
+
 def test_column_info_named():
     s = CompiledSchema(CONFIGS["C3"].chain)
     assert s.n_columns == 7
