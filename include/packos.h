@@ -194,10 +194,15 @@ int packos_encoded_size_batch(const packos_schema* s, const packos_column* cols,
  * is at i*B).  status (n, device) may be NULL.  out_capacity is checked only
  * when offsets are known on the host side (fixed schemas); for variable
  * schemas blobs that would end past out_capacity are not written and get
- * PACKOS_ERR_ENCODE in their status.                                         */
+ * PACKOS_ERR_ENCODE in their status.  Var-width column offsets must be
+ * non-decreasing over all n+1 entries (also for rows inside nil containers).
+ * Offsets that do not match the schema's sizes (a caller-made layout with
+ * gaps) are honoured: such blobs take a per-blob path and gap bytes are
+ * never written.                                                             */
 #define PACKOS_ENC_OFFSETS_READY 1u
-/* testing/benchmark knob: use the general 4-blob-period fixed kernel even
- * when the lane-invariant one applies                                        */
+/* testing/benchmark knob: fixed-size batches use the general 4-blob-period
+ * kernel even when the lane-invariant one applies; variable-size batches use
+ * the one-wavefront-per-blob kernel instead of the tiled one                 */
 #define PACKOS_ENC_FORCE_GENERIC 2u
 /* testing/benchmark knob: pick the fixed-layout kernel variant (0 = auto):
  * 1..4 lane-invariant, dword stores {plain, NT stores, NT loads, NT both};

@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(HERE, "libpackos.so")
 MODE_PUTACCESS = 0
 MODE_PACKABLE = 1
 ENC_OFFSETS_READY = 1
+ENC_FORCE_GENERIC = 2
 
 STATUS_PANIC = 0x40000000
 STATUS_OVERFLOW13 = 0x80000000

@@ -203,7 +203,7 @@ def encode_batch(schema: CompiledSchema, cols: DeviceColumns, want_offsets: bool
         out = torch.empty(max(total, 16), dtype=torch.uint8, device=dev)
     check(L.packos_encode_batch(schema.handle, arr, n, out.data_ptr(), out.numel(), offs.data_ptr(),
                                 None if status is None else status.data_ptr(), ws.data_ptr(), wsb,
-                                _lib.ENC_OFFSETS_READY, st), "packos_encode_batch")
+                                _lib.ENC_OFFSETS_READY | flags, st), "packos_encode_batch")
     return EncodeResult(out, offs, status[:n] if status is not None else None, total, -1)
 
 

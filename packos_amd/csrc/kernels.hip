@@ -468,7 +468,101 @@ __global__ __launch_bounds__(kBlock) void k_scan_add(uint64_t* x, uint64_t n, co
         if (base + k < n) x[base + k] += add;
 }
 
-// pass 2: one wavefront per blob
+// One blob, one wavefront: item sizes -> wavefront prefix scan -> header
+// words -> payload.  `slot` (LDS, kSlot bytes) stages the blob for aligned
+// 16-B stores; with slot == nullptr (or a blob too big for it) bytes go
+// straight to HBM.  `pos` is a per-wave LDS array of n_items + 1 words.
+__device__ void var_blob_wave(const EncProgram& P, const EncCols& cols, uint64_t i, uint64_t o,
+                              uint8_t* __restrict__ out, uint64_t cap, uint32_t* __restrict__ status,
+                              uint8_t* slot, uint32_t* pos, int lane) {
+    const uint64_t pm = present_mask(P, cols, i);
+    // item sizes -> wavefront prefix scan -> positions
+    uint32_t running = 0, slack = 0;
+    for (int b = 0; b < P.n_items; b += kWave) {
+        const int k = b + lane;
+        uint32_t sz = 0;
+        if (k < P.n_items) sz = item_size(P.items[k], cols, i, pm, &slack);
+        const uint32_t incl = wave_incl_scan(sz, lane);
+        if (k < P.n_items) pos[k] = running + incl - sz;
+        running += __shfl(incl, kWave - 1, kWave);
+    }
+    slack = wave_sum(slack);
+    const uint32_t payload_end = running;
+    const uint32_t total = running + (P.mode == PACKOS_MODE_PACKABLE ? slack : 0u);
+    if (lane == 0) pos[P.n_items] = running;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (o + total > cap) {
+        if (status && lane == 0) status[i] = (uint32_t)PACKOS_ERR_ENCODE;
+        __builtin_amdgcn_wave_barrier();
+        return;
+    }
+    const bool staged = slot && total + 16 <= (uint32_t)kSlot;
+    uint8_t* dst = staged ? (slot + (o & 15)) : (out + o);
+
+    // header words (lane per header)
+    bool ovf = false;
+    for (int b = 0; b < P.n_hdrs; b += kWave) {
+        const int k = b + lane;
+        if (k < P.n_hdrs) {
+            const EncHdr h = P.hdrs[k];
+            if ((pm >> h.cont) & 1ull) {
+                const uint32_t hpos = pos[h.hdr_item];
+                uint16_t v;
+                if (h.relative) {
+                    const int64_t off = (int64_t)pos[h.target] - (int64_t)(hpos + P.items[h.hdr_item].size);
+                    ovf |= off >= 8192;
+                    v = enc_header(off, h.tag);
+                } else {
+                    v = h.value;
+                    ovf |= h.ovf != 0;
+                }
+                dst[hpos + 2 * h.j] = (uint8_t)v;
+                dst[hpos + 2 * h.j + 1] = (uint8_t)(v >> 8);
+            }
+        }
+    }
+    // payload bytes (wave per item)
+    for (int k = 0; k < P.n_items; k++) {
+        const EncItem it = P.items[k];
+        if (it.type == IT_HDR) continue;
+        const uint32_t p0 = pos[k], p1 = pos[k + 1];
+        const uint32_t len = p1 - p0;
+        if (len == 0) continue;
+        const uint8_t* src;
+        if (it.type == IT_CONST) src = P.lits + it.lit;
+        else if (it.type == IT_FIXED) src = cols.data[it.col] + i * (uint64_t)it.size;
+        else src = cols.data[it.col] + cols.off[it.col][i];
+        if (it.is_bool) {
+            if (lane == 0) dst[p0] = src[0] != 0;
+        } else {
+            for (uint32_t j = lane; j < len; j += kWave) dst[p0 + j] = src[j];
+        }
+    }
+    // packable.Pack slack: zero bytes after the End-marked payload
+    for (uint32_t j = lane; j < total - payload_end; j += kWave) dst[payload_end + j] = 0;
+    if (staged) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t mis = (uint32_t)(o & 15);
+        const uint32_t head = min(total, (16u - mis) & 15u);
+        if ((uint32_t)lane < head) out[o + lane] = dst[lane];
+        const uint32_t body = (total - head) / 16;
+        const uint8_t* sb = dst + head;              // 16-B aligned in LDS
+        uint8_t* gb = out + o + head;                // 16-B aligned in HBM
+        for (uint32_t c = lane; c < body; c += kWave) *(uint4*)(gb + 16 * c) = *(const uint4*)(sb + 16 * c);
+        const uint32_t done = head + body * 16;
+        if ((uint32_t)lane < total - done) out[o + done + lane] = dst[done + lane];
+        __builtin_amdgcn_wave_barrier();
+    }
+    const bool any_ovf = __ballot(ovf) != 0ull;
+    if (status && lane == 0) status[i] = any_ovf ? PACKOS_STATUS_OVERFLOW13 : 0u;
+    // make sure no lane reuses the slot / pos array before every lane has read it
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// pass 2 (general): one wavefront per blob
 __global__ __launch_bounds__(kBlock) void k_encode_var(EncProgram P, EncCols cols, const uint64_t* __restrict__ offs,
                                                        uint64_t stride, uint8_t* __restrict__ out, uint64_t cap,
                                                        uint64_t n, uint32_t* __restrict__ status) {
@@ -478,95 +572,246 @@ __global__ __launch_bounds__(kBlock) void k_encode_var(EncProgram P, EncCols col
     const int wave_bytes = kSlot + ((npos * 4 + 15) / 16) * 16;
     uint8_t* slot = lds + wave * wave_bytes;
     uint32_t* pos = (uint32_t*)(slot + kSlot);
-
     for (uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + wave; i < n;
-         i += (uint64_t)gridDim.x * kWavesPerBlock) {
-        const uint64_t pm = present_mask(P, cols, i);
-        // item sizes -> wavefront prefix scan -> positions
-        uint32_t running = 0, slack = 0;
-        for (int b = 0; b < P.n_items; b += kWave) {
-            const int k = b + lane;
-            uint32_t sz = 0;
-            if (k < P.n_items) sz = item_size(P.items[k], cols, i, pm, &slack);
-            const uint32_t incl = wave_incl_scan(sz, lane);
-            if (k < P.n_items) pos[k] = running + incl - sz;
-            running += __shfl(incl, kWave - 1, kWave);
+         i += (uint64_t)gridDim.x * kWavesPerBlock)
+        var_blob_wave(P, cols, i, offs ? offs[i] : i * stride, out, cap, status, slot, pos, lane);
+}
+
+// Tiled var-size encode.  A workgroup takes kVT consecutive blobs; their
+// outputs are contiguous in the arena (offsets from the size pass), so the
+// group assembles a run of blobs in LDS and writes it with 16-B stores:
+//   A  per-blob bookkeeping: presence masks, item sizes ((blob, item) pairs,
+//      one thread each), per-blob prefix -> item positions (u16, LDS);
+//   R  split the tile into runs: blobs whose start falls in one kVWin-byte
+//      window (so a run spans < kVBud bytes unless a blob is > kVWin);
+//   B  per run: zero the LDS run buffer, write header words ((blob, header)
+//      pairs), then every item as a byte loop over the run's rows — fixed and
+//      literal items read consecutive column bytes, var items read the
+//      column's contiguous byte range and find their blob by binary search
+//      over the staged column offsets — so global loads are coalesced;
+//   W  16-B non-temporal stores of the run ([start, end) bytes exactly).
+// Tiles the plan does not cover (offsets that disagree with the program, a
+// blob > 64 KiB, capacity overrun) and oversized runs use var_blob_wave.
+constexpr int kVT = 64;            // blobs per tile (== wavefront size)
+constexpr int kVBud = 16384;       // LDS run buffer
+constexpr int kVWin = kVBud / 2;   // run window (power of two)
+
+struct VtLayout {
+    uint32_t boff, pmk, bsz, bst, slk, misc, subs, imag, ivs, voff, pos, total;
+};
+__host__ __device__ inline VtLayout vt_layout(int NI, int nvar) {
+    VtLayout L;
+    uint32_t o = kVBud + 32;
+    L.boff = o; o += 8 * (kVT + 1);
+    L.pmk = o;  o += 8 * kVT;
+    L.bsz = o;  o += 4 * kVT;
+    L.bst = o;  o += 4 * kVT;
+    L.slk = o;  o += 4 * kVT;
+    L.misc = o; o += 4 * 2;
+    L.subs = o; o += 4 * (kVT + 1);
+    L.imag = o; o += 4 * NI;
+    L.ivs = o;  o += (NI + 3) & ~3;
+    L.voff = o; o += 4 * nvar * (kVT + 1);
+    L.pos = o;  o += 2 * kVT * (NI + 1);
+    L.total = (o + 15) & ~15u;
+    return L;
+}
+
+__device__ __forceinline__ uint32_t magic_of(uint32_t d) {
+    return d > 1 ? (uint32_t)((0x100000000ull + d - 1) / d) : 0u;
+}
+__device__ __forceinline__ uint32_t fast_div(uint32_t t, uint32_t d, uint32_t mg) { return d > 1 ? __umulhi(t, mg) : t; }
+
+__global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCols cols,
+                                                            const uint64_t* __restrict__ offs,
+                                                            uint8_t* __restrict__ out, uint64_t cap, uint64_t n,
+                                                            uint32_t* __restrict__ status, int nvar) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int NI = P.n_items, NP = NI + 1, NH = P.n_hdrs;
+    const VtLayout L = vt_layout(NI, nvar);
+    uint8_t* obuf = lds;
+    uint64_t* boff = (uint64_t*)(lds + L.boff);
+    uint64_t* pmk = (uint64_t*)(lds + L.pmk);
+    uint32_t* bsz = (uint32_t*)(lds + L.bsz);
+    uint32_t* bst = (uint32_t*)(lds + L.bst);
+    uint32_t* slk = (uint32_t*)(lds + L.slk);
+    uint32_t* misc = (uint32_t*)(lds + L.misc);
+    uint32_t* subs = (uint32_t*)(lds + L.subs);
+    uint32_t* imag = (uint32_t*)(lds + L.imag);
+    uint8_t* ivs = lds + L.ivs;
+    uint32_t* voff = (uint32_t*)(lds + L.voff);
+    uint16_t* pos = (uint16_t*)(lds + L.pos);
+
+    const uint64_t lo = (uint64_t)blockIdx.x * kVT;
+    const uint32_t rows = (uint32_t)min((uint64_t)kVT, n - lo);
+    const uint32_t ni_mag = magic_of((uint32_t)NI), nh_mag = magic_of((uint32_t)NH);
+
+    for (int k = tid; k < NI; k += kBlock) {
+        const EncItem it = P.items[k];
+        imag[k] = magic_of(it.size);
+        int v = 0;
+        for (int k2 = 0; k2 < k; k2++) v += P.items[k2].type == IT_VAR;
+        ivs[k] = (uint8_t)v;
+    }
+    if (tid == 0) misc[0] = 0;
+    for (uint32_t j = tid; j <= rows; j += kBlock) boff[j] = offs[lo + j];
+    for (uint32_t j = tid; j < rows; j += kBlock) {
+        pmk[j] = present_mask(P, cols, lo + j);
+        slk[j] = 0;
+        bst[j] = 0;
+    }
+    __syncthreads();
+    // A: item sizes
+    for (uint32_t t = tid; t < rows * (uint32_t)NI; t += kBlock) {
+        const uint32_t j = fast_div(t, (uint32_t)NI, ni_mag), k = t - j * (uint32_t)NI;
+        const EncItem it = P.items[k];
+        const uint64_t i = lo + j;
+        const bool present = (pmk[j] >> it.cont) & 1ull;
+        uint32_t sz = 0;
+        if (it.type == IT_VAR) {
+            const uint32_t* o = cols.off[it.col];
+            const uint32_t a = o[i], b = o[i + 1];
+            uint32_t* vo = voff + ivs[k] * (kVT + 1);
+            vo[j] = a;
+            if (j == rows - 1) vo[j + 1] = b;
+            if (present) sz = b - a;
+        } else if (present) {
+            sz = it.size;
+            if (it.type == IT_FIXED && it.nullable) {
+                const uint8_t* v = cols.valid[it.col];
+                if (v && !v[i]) { atomicAdd(&slk[j], it.size); sz = 0; }
+            }
         }
-        slack = wave_sum(slack);
-        const uint32_t payload_end = running;
-        const uint32_t total = running + (P.mode == PACKOS_MODE_PACKABLE ? slack : 0u);
-        if (lane == 0) pos[P.n_items] = running;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        const uint64_t o = offs ? offs[i] : i * stride;
-        if (o + total > cap) {
-            if (status && lane == 0) status[i] = (uint32_t)PACKOS_ERR_ENCODE;
+        if (sz > 0xFFFFu) atomicOr(&misc[0], 1u);
+        pos[j * NP + k] = (uint16_t)sz;
+    }
+    __syncthreads();
+    for (uint32_t j = tid; j < rows; j += kBlock) {
+        uint32_t p = 0;
+        uint16_t* pj = pos + j * NP;
+        for (int k = 0; k < NI; k++) {
+            const uint32_t sz = pj[k];
+            pj[k] = (uint16_t)p;
+            p += sz;
+        }
+        pj[NI] = (uint16_t)p;
+        const uint32_t tot = p + (P.mode == PACKOS_MODE_PACKABLE ? slk[j] : 0u);
+        bsz[j] = tot;
+        if (p > 0xFFFFu || boff[j + 1] - boff[j] != tot || boff[j] + tot > cap) atomicOr(&misc[0], 1u);
+    }
+    __syncthreads();
+    if (misc[0]) {  // outside the tile plan: one wavefront per blob, straight to HBM
+        uint32_t* wpos = (uint32_t*)obuf + wave * NP;
+        for (uint32_t j = wave; j < rows; j += kWavesPerBlock)
+            var_blob_wave(P, cols, lo + j, boff[j], out, cap, status, nullptr, wpos, lane);
+        return;
+    }
+    // R: runs of blobs whose start offsets share a kVWin window
+    if (wave == 0) {
+        const uint32_t win = (uint32_t)((boff[min((uint32_t)lane, rows - 1)] - boff[0]) / kVWin);
+        const uint32_t prev = __shfl_up(win, 1, kWave);
+        const bool isnew = (uint32_t)lane < rows && (lane == 0 || win != prev);
+        const uint64_t bal = __ballot(isnew);
+        if (isnew) subs[__popcll(bal & ((1ull << lane) - 1ull))] = lane;
+        if (lane == 0) {
+            misc[1] = (uint32_t)__popcll(bal);
+            subs[__popcll(bal)] = rows;
+        }
+    }
+    __syncthreads();
+    const uint32_t nsub = misc[1];
+    for (uint32_t q = 0; q < nsub; q++) {
+        const uint32_t a = subs[q], b = subs[q + 1];
+        const uint64_t s0 = boff[a], s1 = boff[b];
+        const uint64_t al = s0 & ~15ull;
+        const uint32_t nb = (uint32_t)(s1 - al);
+        if (nb + 16 > (uint32_t)kVBud) {
+            uint32_t* wpos = (uint32_t*)obuf + wave * NP;
+            for (uint32_t j = a + wave; j < b; j += kWavesPerBlock)
+                var_blob_wave(P, cols, lo + j, boff[j], out, cap, status, nullptr, wpos, lane);
+            for (uint32_t j = a + tid; j < b; j += kBlock) bst[j] = 2u;  // status already written
+            __syncthreads();
             continue;
         }
-        const bool staged = total + 16 <= (uint32_t)kSlot;
-        uint8_t* dst = staged ? (slot + (o & 15)) : (out + o);
-
-        // header words (lane per header)
-        bool ovf = false;
-        for (int b = 0; b < P.n_hdrs; b += kWave) {
-            const int k = b + lane;
-            if (k < P.n_hdrs) {
-                const EncHdr h = P.hdrs[k];
-                if ((pm >> h.cont) & 1ull) {
-                    const uint32_t hpos = pos[h.hdr_item];
-                    uint16_t v;
-                    if (h.relative) {
-                        const int64_t off = (int64_t)pos[h.target] - (int64_t)(hpos + P.items[h.hdr_item].size);
-                        ovf |= off >= 8192;
-                        v = enc_header(off, h.tag);
-                    } else {
-                        v = h.value;
-                        ovf |= h.ovf != 0;
+        const uint32_t nch = (nb + 15) >> 4;
+        for (uint32_t c = tid; c < nch; c += kBlock) ((u32x4*)obuf)[c] = u32x4{0u, 0u, 0u, 0u};
+        __syncthreads();
+        // header words
+        for (uint32_t t = tid; t < (b - a) * (uint32_t)NH; t += kBlock) {
+            const uint32_t jj = fast_div(t, (uint32_t)NH, nh_mag), hh = t - jj * (uint32_t)NH;
+            const uint32_t j = a + jj;
+            const EncHdr h = P.hdrs[hh];
+            if (!((pmk[j] >> h.cont) & 1ull)) continue;
+            const uint16_t* pj = pos + j * NP;
+            const uint32_t hpos = pj[h.hdr_item];
+            uint16_t v;
+            bool ovf;
+            if (h.relative) {
+                const int64_t off = (int64_t)pj[h.target] - (int64_t)(hpos + P.items[h.hdr_item].size);
+                ovf = off >= 8192;
+                v = enc_header(off, h.tag);
+            } else {
+                v = h.value;
+                ovf = h.ovf != 0;
+            }
+            if (ovf) atomicOr(&bst[j], 1u);
+            const uint32_t d = (uint32_t)(boff[j] - al) + hpos + 2 * h.j;
+            obuf[d] = (uint8_t)v;
+            obuf[d + 1] = (uint8_t)(v >> 8);
+        }
+        // items
+        for (int k = 0; k < NI; k++) {
+            const EncItem it = P.items[k];
+            if (it.type == IT_HDR) continue;
+            if (it.type != IT_VAR) {
+                const uint32_t w = it.size, mg = imag[k];
+                const bool lit = it.type == IT_CONST;
+                const uint8_t* src = lit ? P.lits + it.lit : cols.data[it.col] + (lo + a) * (uint64_t)w;
+                for (uint32_t t = tid; t < (b - a) * w; t += kBlock) {
+                    const uint32_t jj = fast_div(t, w, mg), bb = t - jj * w;
+                    const uint32_t j = a + jj;
+                    const uint16_t* pj = pos + j * NP;
+                    const uint32_t p0 = pj[k];
+                    if (pj[k + 1] == p0) continue;  // absent (nil leaf or container)
+                    uint32_t x = lit ? src[bb] : src[t];
+                    if (it.is_bool) x = x != 0;
+                    obuf[(uint32_t)(boff[j] - al) + p0 + bb] = (uint8_t)x;
+                }
+            } else {
+                const uint32_t* vo = voff + ivs[k] * (kVT + 1);
+                const uint32_t v0 = vo[a], v1 = vo[b];
+                const uint8_t* src = cols.data[it.col];
+                for (uint32_t t = v0 + tid; t < v1; t += kBlock) {
+                    uint32_t l = a, r = b - 1;  // last blob j with vo[j] <= t
+                    while (l < r) {
+                        const uint32_t m = (l + r + 1) >> 1;
+                        if (vo[m] <= t) l = m; else r = m - 1;
                     }
-                    dst[hpos + 2 * h.j] = (uint8_t)v;
-                    dst[hpos + 2 * h.j + 1] = (uint8_t)(v >> 8);
+                    const uint16_t* pj = pos + l * NP;
+                    const uint32_t p0 = pj[k], rel = t - vo[l];
+                    if (rel < (uint32_t)(pj[k + 1] - p0)) obuf[(uint32_t)(boff[l] - al) + p0 + rel] = src[t];
                 }
             }
         }
-        // payload bytes (wave per item)
-        for (int k = 0; k < P.n_items; k++) {
-            const EncItem it = P.items[k];
-            if (it.type == IT_HDR) continue;
-            const uint32_t p0 = pos[k], p1 = pos[k + 1];
-            const uint32_t len = p1 - p0;
-            if (len == 0) continue;
-            const uint8_t* src;
-            if (it.type == IT_CONST) src = P.lits + it.lit;
-            else if (it.type == IT_FIXED) src = cols.data[it.col] + i * (uint64_t)it.size;
-            else src = cols.data[it.col] + cols.off[it.col][i];
-            if (it.is_bool) {
-                if (lane == 0) dst[p0] = src[0] != 0;
+        __syncthreads();
+        // write [s0, s1)
+        for (uint32_t c = tid; c < nch; c += kBlock) {
+            const uint64_t g0 = al + 16ull * c;
+            if (g0 >= s0 && g0 + 16 <= s1) {
+                __builtin_nontemporal_store(((const u32x4*)obuf)[c], (u32x4*)(out + g0));
             } else {
-                for (uint32_t j = lane; j < len; j += kWave) dst[p0 + j] = src[j];
+                for (int x = 0; x < 16; x++) {
+                    const uint64_t g = g0 + x;
+                    if (g >= s0 && g < s1) out[g] = obuf[16 * c + x];
+                }
             }
         }
-        // packable.Pack slack: zero bytes after the End-marked payload
-        for (uint32_t j = lane; j < total - payload_end; j += kWave) dst[payload_end + j] = 0;
-        if (staged) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            const uint32_t mis = (uint32_t)(o & 15);
-            const uint32_t head = min(total, (16u - mis) & 15u);
-            if ((uint32_t)lane < head) out[o + lane] = dst[lane];
-            const uint32_t body = (total - head) / 16;
-            const uint8_t* sb = dst + head;              // 16-B aligned in LDS
-            uint8_t* gb = out + o + head;                // 16-B aligned in HBM
-            for (uint32_t c = lane; c < body; c += kWave) *(uint4*)(gb + 16 * c) = *(const uint4*)(sb + 16 * c);
-            const uint32_t done = head + body * 16;
-            if ((uint32_t)lane < total - done) out[o + done + lane] = dst[done + lane];
-            __builtin_amdgcn_wave_barrier();
-        }
-        const bool any_ovf = __ballot(ovf) != 0ull;
-        if (status && lane == 0) status[i] = any_ovf ? PACKOS_STATUS_OVERFLOW13 : 0u;
-        // make sure no lane reuses the slot before every lane has read it
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        __syncthreads();
     }
+    if (status)
+        for (uint32_t j = tid; j < rows; j += kBlock)
+            if (!(bst[j] & 2u)) status[lo + j] = (bst[j] & 1u) ? PACKOS_STATUS_OVERFLOW13 : 0u;
 }
 
 // =========================================================================
@@ -1243,6 +1488,17 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
         return PACKOS_E_INVALID;
     }
     const size_t npos = s->items.size() + 1;
+    int nvar = 0;
+    for (const EncItem& it : s->items) nvar += it.type == IT_VAR;
+    const VtLayout vl = vt_layout((int)s->items.size(), nvar);
+    const bool tiled = !(flags & PACKOS_ENC_FORCE_GENERIC) && vl.total <= 64 * 1024 && nvar < 256 &&
+                       npos * 4 * kWavesPerBlock <= (size_t)kVBud;
+    if (tiled) {
+        hipLaunchKernelGGL(k_encode_var_tile, dim3((unsigned)((n + kVT - 1) / kVT)), dim3(kBlock), (size_t)vl.total,
+                           st, t->enc, ec, (const uint64_t*)out_offsets, out, cap, (uint64_t)n, status, nvar);
+        HIP_TRY(hipGetLastError());
+        return PACKOS_OK;
+    }
     const size_t lds = (size_t)kWavesPerBlock * (kSlot + ((npos * 4 + 15) / 16) * 16);
     if (lds > 64 * 1024) { set_error("schema has too many items for the LDS budget"); return PACKOS_E_UNSUPPORTED; }
     const unsigned grid = (unsigned)std::min<uint64_t>((n + kWavesPerBlock - 1) / kWavesPerBlock, 256 * 16);

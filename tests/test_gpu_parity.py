@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import oracle_bridge as ob
+from packos_amd import _lib
 from golden_util import MODES, chain_of, load, unwrap
 from packos_amd.api import CompiledSchema, DeviceColumns, decode_batch, encode_batch, get_field_batch
 from packos_amd.columns import HostColumns
@@ -24,11 +25,11 @@ def torch():
     return t
 
 
-def gpu_encode(chain, hc, mode=0):
+def gpu_encode(chain, hc, mode=0, flags=0):
     T = torch()
     s = CompiledSchema(chain, mode)
     dc = DeviceColumns.from_host(s, hc, "cuda:0")
-    r = encode_batch(s, dc)
+    r = encode_batch(s, dc, flags=flags)
     T.cuda.synchronize()
     arena = r.arena[: r.total].cpu().numpy()
     offs = r.offsets.cpu().numpy().astype(np.uint64)
@@ -36,9 +37,9 @@ def gpu_encode(chain, hc, mode=0):
     return arena, offs, st
 
 
-def assert_same_encoding(chain, hc, mode, what=""):
+def assert_same_encoding(chain, hc, mode, what="", flags=0):
     a0, o0, s0 = ob.encode(chain, hc, mode, nthreads=8)
-    a1, o1, s1 = gpu_encode(chain, hc, mode)
+    a1, o1, s1 = gpu_encode(chain, hc, mode, flags)
     assert np.array_equal(o0, o1), f"{what}: offsets differ"
     if not np.array_equal(a0, a1):
         bad = int(np.nonzero(a0 != a1)[0][0])
@@ -74,6 +75,56 @@ def test_random_schema_encode(seed, mode):
     chain = rand_chain(seed)
     hc = HostColumns.from_rows(chain, rand_rows(chain, 257, seed * 7 + 1))
     assert_same_encoding(chain, hc, mode, f"seed {seed}")
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("seed", range(20))
+def test_random_schema_encode_wave_kernel(seed, mode):
+    # PACKOS_ENC_FORCE_GENERIC: the one-wavefront-per-blob kernel (the tiled
+    # kernel's fallback) on its own
+    chain = rand_chain(seed)
+    hc = HostColumns.from_rows(chain, rand_rows(chain, 257, seed * 7 + 1))
+    assert_same_encoding(chain, hc, mode, f"wave seed {seed}", flags=_lib.ENC_FORCE_GENERIC)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_var_tile_runs_and_fallbacks(mode):
+    """Tiled var encode: runs split at 8 KiB windows, runs larger than the LDS
+    budget, blobs > 64 KiB (whole-tile fallback), and ragged last tiles."""
+    chain = SChain(SInt16, SVariableString(), STuple(SVariableString(), SInt16))
+    rng = np.random.default_rng(5)
+    rows = []
+    for i in range(333):
+        r = rng.random()
+        ln = int(rng.integers(0, 40)) if r < 0.7 else int(rng.integers(3000, 12000)) if r < 0.97 else 70_000
+        rows.append([i, "s" * ln, None if rng.random() < 0.1 else ["t" * int(rng.integers(0, 300)), -i]])
+    hc = HostColumns.from_rows(chain, rows)
+    assert_same_encoding(chain, hc, mode, "tile edges")
+
+
+def test_var_encode_capacity_overrun():
+    T = torch()
+    cfg = CONFIGS["C3"]
+    hc = make_columns(cfg, n=5000)
+    a0, o0, _ = ob.encode(cfg.chain, hc, 0, nthreads=8)
+    s = CompiledSchema(cfg.chain, 0)
+    dc = DeviceColumns.from_host(s, hc, "cuda:0")
+    L = _lib.lib()
+    n = hc.n
+    cap = int(o0[n]) - 1000
+    out = T.zeros(cap, dtype=T.uint8, device="cuda:0")
+    offs = T.empty(n + 1, dtype=T.int64, device="cuda:0")
+    st = T.empty(n, dtype=T.int32, device="cuda:0")
+    wsb = L.packos_encode_workspace_size(s.handle, n)
+    ws = T.empty(wsb, dtype=T.uint8, device="cuda:0")
+    assert L.packos_encode_batch(s.handle, dc.ctypes_array(), n, out.data_ptr(), cap, offs.data_ptr(),
+                                 st.data_ptr(), ws.data_ptr(), wsb, 0, None) == 0
+    T.cuda.synchronize()
+    fits = o0[1:] <= cap
+    stn = st.cpu().numpy()
+    assert (stn[fits] == 0).all() and (stn[~fits] == 4).all()
+    last = int(o0[int(fits.sum())])
+    assert np.array_equal(out.cpu().numpy()[:last], a0[:last])
 
 
 @pytest.mark.parametrize("seed", range(30))
