@@ -311,6 +311,13 @@ struct Builder {
         }
         emit_container(0, 0);
         if (s->items.size() > 65000) fail(PACKOS_E_UNSUPPORTED, "schema too large");
+        // per-item kernel aux data: var slot, staging region, divide magic
+        int nv = 0, nr = 0;
+        for (EncItem& it : s->items) {
+            it.vslot = it.type == IT_VAR ? (uint8_t)std::min(nv++, 255) : 0;
+            it.reg = it.type == IT_FIXED ? (uint8_t)std::min(nr++, 255) : 255;
+            it.magic = it.size > 1 ? (uint32_t)(((1ull << 32) + it.size - 1) / it.size) : 0u;
+        }
     }
 
     // All-present blob layout for schemas without var leaves.

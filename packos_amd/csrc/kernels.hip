@@ -577,43 +577,76 @@ __global__ __launch_bounds__(kBlock) void k_encode_var(EncProgram P, EncCols col
         var_blob_wave(P, cols, i, offs ? offs[i] : i * stride, out, cap, status, slot, pos, lane);
 }
 
-// Tiled var-size encode.  A workgroup takes kVT consecutive blobs; their
+// Tiled var-size encode.  A workgroup takes VT consecutive blobs; their
 // outputs are contiguous in the arena (offsets from the size pass), so the
-// group assembles a run of blobs in LDS and writes it with 16-B stores:
-//   A  per-blob bookkeeping: presence masks, item sizes ((blob, item) pairs,
-//      one thread each), per-blob prefix -> item positions (u16, LDS);
-//   R  split the tile into runs: blobs whose start falls in one kVWin-byte
-//      window (so a run spans < kVBud bytes unless a blob is > kVWin);
-//   B  per run: zero the LDS run buffer, write header words ((blob, header)
-//      pairs), then every item as a byte loop over the run's rows — fixed and
-//      literal items read consecutive column bytes, var items read the
-//      column's contiguous byte range and find their blob by binary search
-//      over the staged column offsets — so global loads are coalesced;
-//   W  16-B non-temporal stores of the run ([start, end) bytes exactly).
-// Tiles the plan does not cover (offsets that disagree with the program, a
-// blob > 64 KiB, capacity overrun) and oversized runs use var_blob_wave.
-constexpr int kVT = 64;            // blobs per tile (== wavefront size)
-constexpr int kVBud = 16384;       // LDS run buffer
-constexpr int kVWin = kVBud / 2;   // run window (power of two)
+// group assembles runs of blobs in LDS and writes them with 16-B stores.
+// Global-memory latency, not bandwidth, is what a per-blob design pays for,
+// so the kernel is organised in two rounds of independent loads:
+//   round 1  everything that depends only on kernel arguments, issued
+//            together: the schema program (items, header words, containers,
+//            literals), the tile's blob offsets, var-column offsets,
+//            validity bytes and every fixed column's rows (16-B chunks) —
+//            one flattened index space, kVBatch loads in flight per thread;
+//   round 2  the var columns' byte ranges (now known) are staged while the
+//            threads compute presence masks and item positions (LDS only);
+//   runs     the tile is split into runs (blobs whose start falls in one
+//            2^win_shift-byte window); per run the LDS buffer is zeroed,
+//            header words and items are written by (header|item, blob) pairs
+//            from LDS, and the run is stored with 16-B non-temporal stores;
+//   direct   var values that did not fit the staging budget (long values)
+//            are copied HBM->HBM afterwards, flattened over destination
+//            dwords so that every thread keeps several loads in flight.
+// Tiles outside the plan (offsets that disagree with the program, a blob
+// > 64 KiB, capacity overrun) and runs > bud bytes use var_blob_wave.
+constexpr int kVBatch = 8;
+constexpr int kVPFix = 32;     // plan limits (more -> one wavefront per blob)
+constexpr int kVPVar = 16;
+constexpr int kVPVal = 16;
+
+struct VarPlan {               // per-call plan, passed by value
+    int32_t nfix, nvar, nval, fix_bytes;
+    const uint8_t* fix_ptr[kVPFix];   // fixed leaf columns (one region per IT_FIXED item)
+    uint32_t fix_w[kVPFix];
+    uint32_t fix_lds[kVPFix];  // staging offset of fixed region r (full tile, 16-B aligned)
+    const uint32_t* var_off[kVPVar];  // var leaf columns (one per IT_VAR item)
+    const uint8_t* var_data[kVPVar];
+    int32_t var_item[kVPVar];
+    const uint8_t* val_ptr[kVPVal];   // validity columns passed by the caller
+    int8_t col_val[kMaxCols];  // column -> validity slot, -1 none
+};
+
+struct VVar {                  // var region of the current tile (LDS)
+    uint64_t src;              // column bytes of the tile's first blob
+    uint32_t lds_off;          // staging offset, UINT32_MAX = not staged
+    uint32_t pad;
+};
 
 struct VtLayout {
-    uint32_t boff, pmk, bsz, bst, slk, misc, subs, imag, ivs, voff, pos, total;
+    uint32_t boff, pmk, bst, misc, subs, items, hdrs, conts, lits, voff, vld, pos, vvar, fmis, skip, stg, total;
 };
-__host__ __device__ inline VtLayout vt_layout(int NI, int nvar) {
+__host__ __device__ inline VtLayout vt_layout(int VT, const EncProgram& P, int nvar, int nval, uint32_t bud,
+                                               uint32_t in_bud) {
+    auto al16 = [](uint32_t x) { return (x + 15u) & ~15u; };
+    const uint32_t NI = (uint32_t)P.n_items;
     VtLayout L;
-    uint32_t o = kVBud + 32;
-    L.boff = o; o += 8 * (kVT + 1);
-    L.pmk = o;  o += 8 * kVT;
-    L.bsz = o;  o += 4 * kVT;
-    L.bst = o;  o += 4 * kVT;
-    L.slk = o;  o += 4 * kVT;
-    L.misc = o; o += 4 * 2;
-    L.subs = o; o += 4 * (kVT + 1);
-    L.imag = o; o += 4 * NI;
-    L.ivs = o;  o += (NI + 3) & ~3;
-    L.voff = o; o += 4 * nvar * (kVT + 1);
-    L.pos = o;  o += 2 * kVT * (NI + 1);
-    L.total = (o + 15) & ~15u;
+    uint32_t o = al16(bud + 32);
+    L.boff = o;  o += 8 * (VT + 1);
+    L.pmk = o;   o += 8 * VT;
+    L.bst = o;   o += 4 * VT;
+    L.misc = o;  o += 4 * 16;
+    L.subs = o;  o += al16(4 * (VT + 1));
+    L.items = o; o += al16(sizeof(EncItem) * NI);
+    L.hdrs = o;  o += al16(sizeof(EncHdr) * (uint32_t)P.n_hdrs);
+    L.conts = o; o += al16(sizeof(EncCont) * (uint32_t)P.n_conts);
+    L.lits = o;  o += al16((uint32_t)P.n_lits + 4);
+    L.voff = o;  o += 4 * nvar * (VT + 1);
+    L.vld = o;   o += al16(nval * VT);
+    L.pos = o;   o += al16(2 * VT * (NI + 1));
+    L.vvar = o;  o += al16(sizeof(VVar) * nvar);
+    L.fmis = o;  o += al16(4 * kVPFix);
+    L.skip = o;  o += al16(4 * ((bud + 32) / 16 / 32 + 1));
+    L.stg = o;   o += al16(in_bud + 16);
+    L.total = o;
     return L;
 }
 
@@ -622,133 +655,300 @@ __device__ __forceinline__ uint32_t magic_of(uint32_t d) {
 }
 __device__ __forceinline__ uint32_t fast_div(uint32_t t, uint32_t d, uint32_t mg) { return d > 1 ? __umulhi(t, mg) : t; }
 
-__global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCols cols,
+typedef __attribute__((address_space(1))) const uint32_t g_u32;
+typedef __attribute__((address_space(1))) const uint64_t g_u64;
+typedef __attribute__((address_space(1))) const uint8_t g_u8;
+
+template <int VT>
+__global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCols cols, VarPlan V,
                                                             const uint64_t* __restrict__ offs,
                                                             uint8_t* __restrict__ out, uint64_t cap, uint64_t n,
-                                                            uint32_t* __restrict__ status, int nvar) {
+                                                            uint32_t* __restrict__ status, uint32_t bud,
+                                                            uint32_t win_shift, uint32_t in_bud,
+                                                            uint32_t* __restrict__ tflags, uint16_t* __restrict__ vpos,
+                                                            unsigned long long* __restrict__ prof) {
+    static_assert(VT % kWave == 0 && VT <= kBlock, "tile = whole wavefronts, at most one blob per thread");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int NI = P.n_items, NP = NI + 1, NH = P.n_hdrs;
-    const VtLayout L = vt_layout(NI, nvar);
+    const VtLayout L = vt_layout(VT, P, V.nvar, V.nval, bud, in_bud);
     uint8_t* obuf = lds;
     uint64_t* boff = (uint64_t*)(lds + L.boff);
     uint64_t* pmk = (uint64_t*)(lds + L.pmk);
-    uint32_t* bsz = (uint32_t*)(lds + L.bsz);
     uint32_t* bst = (uint32_t*)(lds + L.bst);
-    uint32_t* slk = (uint32_t*)(lds + L.slk);
-    uint32_t* misc = (uint32_t*)(lds + L.misc);
+    uint32_t* misc = (uint32_t*)(lds + L.misc);   // 0 fallback, 1 #runs, 4..7 wave counts, 8.. scratch
     uint32_t* subs = (uint32_t*)(lds + L.subs);
-    uint32_t* imag = (uint32_t*)(lds + L.imag);
-    uint8_t* ivs = lds + L.ivs;
+    EncItem* items = (EncItem*)(lds + L.items);
+    EncHdr* hdrs = (EncHdr*)(lds + L.hdrs);
+    EncCont* conts = (EncCont*)(lds + L.conts);
+    uint8_t* lits = lds + L.lits;
     uint32_t* voff = (uint32_t*)(lds + L.voff);
+    uint8_t* vld = lds + L.vld;
     uint16_t* pos = (uint16_t*)(lds + L.pos);
+    VVar* vvar = (VVar*)(lds + L.vvar);
+    uint32_t* fmis = (uint32_t*)(lds + L.fmis);
+    uint32_t* skip = (uint32_t*)(lds + L.skip);   // run chunks k_var_copy writes
+    uint8_t* stg = lds + L.stg;
 
-    const uint64_t lo = (uint64_t)blockIdx.x * kVT;
-    const uint32_t rows = (uint32_t)min((uint64_t)kVT, n - lo);
-    const uint32_t ni_mag = magic_of((uint32_t)NI), nh_mag = magic_of((uint32_t)NH);
+    const uint64_t lo = (uint64_t)blockIdx.x * VT;
+    const uint32_t rows = (uint32_t)min((uint64_t)VT, n - lo);
+    uint64_t t_last = prof ? __builtin_amdgcn_s_memtime() : 0;
+    auto mark = [&](int ph) {
+        if (prof && tid == 0) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            atomicAdd(prof + ph, (unsigned long long)(t - t_last));
+            t_last = t;
+        }
+    };
 
-    for (int k = tid; k < NI; k += kBlock) {
-        const EncItem it = P.items[k];
-        imag[k] = magic_of(it.size);
-        int v = 0;
-        for (int k2 = 0; k2 < k; k2++) v += P.items[k2].type == IT_VAR;
-        ivs[k] = (uint8_t)v;
-    }
-    if (tid == 0) misc[0] = 0;
-    for (uint32_t j = tid; j <= rows; j += kBlock) boff[j] = offs[lo + j];
-    for (uint32_t j = tid; j < rows; j += kBlock) {
-        pmk[j] = present_mask(P, cols, lo + j);
-        slk[j] = 0;
-        bst[j] = 0;
-    }
-    __syncthreads();
-    // A: item sizes
-    for (uint32_t t = tid; t < rows * (uint32_t)NI; t += kBlock) {
-        const uint32_t j = fast_div(t, (uint32_t)NI, ni_mag), k = t - j * (uint32_t)NI;
-        const EncItem it = P.items[k];
-        const uint64_t i = lo + j;
-        const bool present = (pmk[j] >> it.cont) & 1ull;
-        uint32_t sz = 0;
-        if (it.type == IT_VAR) {
-            const uint32_t* o = cols.off[it.col];
-            const uint32_t a = o[i], b = o[i + 1];
-            uint32_t* vo = voff + ivs[k] * (kVT + 1);
-            vo[j] = a;
-            if (j == rows - 1) vo[j + 1] = b;
-            if (present) sz = b - a;
-        } else if (present) {
-            sz = it.size;
-            if (it.type == IT_FIXED && it.nullable) {
-                const uint8_t* v = cols.valid[it.col];
-                if (v && !v[i]) { atomicAdd(&slk[j], it.size); sz = 0; }
+    // ---- round 1 -----------------------------------------------------------
+    // one flattened index space; the var-offset and validity segments are
+    // padded to whole wavefronts so the column behind an element is
+    // wave-uniform (scalar pointer loads, no dependent vector loads)
+    {
+        auto al64 = [](uint32_t x) { return (x + 63u) & ~63u; };
+        const uint32_t e_items = (uint32_t)NI * (sizeof(EncItem) / 4);
+        const uint32_t e_hdrs = e_items + (uint32_t)NH * (sizeof(EncHdr) / 4);
+        const uint32_t e_conts = e_hdrs + (uint32_t)P.n_conts * (sizeof(EncCont) / 4);
+        const uint32_t e_lits = e_conts + ((uint32_t)P.n_lits + 3) / 4;
+        const uint32_t e_boff = e_lits + rows + 1;
+        const uint32_t s_voff = al64(e_boff), S1 = al64(rows + 1);
+        const uint32_t e_voff = s_voff + (uint32_t)V.nvar * S1;
+        const uint32_t S0 = al64(rows);
+        const uint32_t e_vld = e_voff + (uint32_t)V.nval * S0;
+        uint32_t fix_ch = 0;
+        for (int r = 0; r < V.nfix; r++) {
+            const uint64_t src = (uint64_t)(uintptr_t)(V.fix_ptr[r] + lo * V.fix_w[r]);
+            if (tid == 0) fmis[r] = V.fix_lds[r] + (uint32_t)(src & 15);
+            fix_ch += (uint32_t)(((src & 15) + (uint64_t)rows * V.fix_w[r] + 15) >> 4);
+        }
+        const uint32_t E = e_vld + fix_ch;
+        for (uint32_t e0 = tid; e0 < E; e0 += kVBatch * kBlock) {
+            u32x4 v[kVBatch];
+            uint32_t dst[kVBatch], kind[kVBatch];  // kind: 1 dword, 2 qword, 3 byte, 4 16-B chunk
+#pragma unroll
+            for (int m = 0; m < kVBatch; m++) {
+                const uint32_t e = e0 + m * kBlock;
+                kind[m] = 0;
+                dst[m] = 0;
+                v[m] = u32x4{0u, 0u, 0u, 0u};
+                if (e >= E) continue;
+                if (e < e_lits) {
+                    const uint32_t* src;
+                    uint32_t x;
+                    if (e < e_items) { src = (const uint32_t*)P.items; x = e; dst[m] = L.items + 4 * x; }
+                    else if (e < e_hdrs) { src = (const uint32_t*)P.hdrs; x = e - e_items; dst[m] = L.hdrs + 4 * x; }
+                    else if (e < e_conts) { src = (const uint32_t*)P.conts; x = e - e_hdrs; dst[m] = L.conts + 4 * x; }
+                    else { src = (const uint32_t*)P.lits; x = e - e_conts; dst[m] = L.lits + 4 * x; }
+                    v[m].x = ((g_u32*)src)[x];
+                    kind[m] = 1;
+                } else if (e < e_boff) {
+                    const uint32_t j = e - e_lits;
+                    const uint64_t o = ((g_u64*)offs)[lo + j];
+                    v[m].x = (uint32_t)o;
+                    v[m].y = (uint32_t)(o >> 32);
+                    dst[m] = L.boff + 8 * j;
+                    kind[m] = 2;
+                } else if (e < s_voff) {
+                    continue;
+                } else if (e < e_voff) {
+                    const uint32_t x = e - s_voff;
+                    const uint32_t vv = __builtin_amdgcn_readfirstlane(x / S1), j = x - vv * S1;
+                    if (j > rows) continue;
+                    v[m].x = ((g_u32*)V.var_off[vv])[lo + j];
+                    dst[m] = L.voff + 4 * (vv * (VT + 1) + j);
+                    kind[m] = 1;
+                } else if (e < e_vld) {
+                    const uint32_t x = e - e_voff;
+                    const uint32_t vv = __builtin_amdgcn_readfirstlane(x / S0), j = x - vv * S0;
+                    if (j >= rows) continue;
+                    v[m].x = ((g_u8*)V.val_ptr[vv])[lo + j];
+                    dst[m] = L.vld + vv * VT + j;
+                    kind[m] = 3;
+                } else {
+                    const uint32_t c = e - e_vld;
+                    uint64_t a0 = 0;
+                    uint32_t cb = 0, base = 0, sel_lds = 0;
+                    for (int r = 0; r < V.nfix; r++) {
+                        const uint64_t src = (uint64_t)(uintptr_t)(V.fix_ptr[r] + lo * V.fix_w[r]);
+                        const uint32_t nch = (uint32_t)(((src & 15) + (uint64_t)rows * V.fix_w[r] + 15) >> 4);
+                        const bool in = c >= base;
+                        a0 = in ? (src & ~15ull) : a0;
+                        cb = in ? base : cb;
+                        sel_lds = in ? V.fix_lds[r] : sel_lds;
+                        base += nch;
+                    }
+                    v[m] = *(const g_u32x4*)(uintptr_t)(a0 + 16ull * (c - cb));
+                    dst[m] = L.stg + sel_lds + 16 * (c - cb);
+                    kind[m] = 4;
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < kVBatch; m++) {
+                switch (kind[m]) {
+                    case 1: *(uint32_t*)(lds + dst[m]) = v[m].x; break;
+                    case 2: *(uint64_t*)(lds + dst[m]) = ((uint64_t)v[m].y << 32) | v[m].x; break;
+                    case 3: lds[dst[m]] = (uint8_t)v[m].x; break;
+                    case 4: *(u32x4*)(lds + dst[m]) = v[m]; break;
+                    default: break;
+                }
             }
         }
-        if (sz > 0xFFFFu) atomicOr(&misc[0], 1u);
-        pos[j * NP + k] = (uint16_t)sz;
+        if (tid < 16) misc[tid] = 0;
     }
     __syncthreads();
+    mark(0);
+    // ---- round 2: var staging plan + loads, positions while they fly --------
+    uint32_t any_direct = 0, vch = 0;
+    {
+        uint32_t used = (uint32_t)V.fix_bytes;
+        for (int vv = 0; vv < V.nvar; vv++) {
+            const uint32_t* vo = voff + vv * (VT + 1);
+            const uint64_t src = (uint64_t)(uintptr_t)(V.var_data[vv] + vo[0]);
+            const uint32_t bytes = vo[rows] - vo[0];
+            const uint32_t nch = bytes ? (uint32_t)(((src & 15) + bytes + 15) >> 4) : 0u;
+            const bool st = used + 16 * nch <= in_bud;
+            if (tid == 0) vvar[vv] = VVar{src, st ? used : UINT32_MAX, 0};
+            if (st) { used += 16 * nch; vch += nch; } else any_direct = 1;
+        }
+    }
+    u32x4 vb[kVBatch];
+    uint32_t vdst[kVBatch];
+    auto var_load = [&](uint32_t c0) {
+#pragma unroll
+        for (int m = 0; m < kVBatch; m++) {
+            const uint32_t c = c0 + m * kBlock;
+            uint64_t a0 = 0;
+            uint32_t cb = 0, base = 0, sl = 0, u2 = (uint32_t)V.fix_bytes;
+            for (int vv = 0; vv < V.nvar; vv++) {
+                const uint32_t* vo = voff + vv * (VT + 1);
+                const uint64_t src = (uint64_t)(uintptr_t)(V.var_data[vv] + vo[0]);
+                const uint32_t bytes = vo[rows] - vo[0];
+                const uint32_t nch = bytes ? (uint32_t)(((src & 15) + bytes + 15) >> 4) : 0u;
+                if (u2 + 16 * nch > in_bud) continue;  // not staged (same rule as the plan)
+                const bool in = c >= base;
+                a0 = in ? (src & ~15ull) : a0;
+                cb = in ? base : cb;
+                sl = in ? u2 : sl;
+                base += nch;
+                u2 += 16 * nch;
+            }
+            vdst[m] = sl + 16 * (c - cb);
+            if (c < vch) vb[m] = *(const g_u32x4*)(uintptr_t)(a0 + 16ull * (c - cb));
+        }
+    };
+    auto var_store = [&](uint32_t c0) {
+#pragma unroll
+        for (int m = 0; m < kVBatch; m++)
+            if (c0 + m * kBlock < vch) *(u32x4*)(stg + vdst[m]) = vb[m];
+    };
+    var_load(tid);
+    // presence masks and item positions (LDS only)
     for (uint32_t j = tid; j < rows; j += kBlock) {
-        uint32_t p = 0;
+        uint64_t pm = 0;
+        for (int c = 0; c < P.n_conts; c++) {
+            const EncCont ct = conts[c];
+            bool p = ct.parent < 0 ? true : ((pm >> ct.parent) & 1ull);
+            if (p && ct.valid_col >= 0) {
+                const int vs = V.col_val[ct.valid_col];
+                if (vs >= 0) p = vld[vs * VT + j] != 0;
+            }
+            if (p) pm |= 1ull << c;
+        }
+        pmk[j] = pm;
+        bst[j] = 0;
+        uint32_t p = 0, slack = 0;
         uint16_t* pj = pos + j * NP;
         for (int k = 0; k < NI; k++) {
-            const uint32_t sz = pj[k];
+            const EncItem it = items[k];
+            uint32_t sz = 0;
+            if ((pm >> it.cont) & 1ull) {
+                if (it.type == IT_VAR) {
+                    const uint32_t* vo = voff + it.vslot * (VT + 1);
+                    sz = vo[j + 1] - vo[j];
+                } else {
+                    sz = it.size;
+                    if (it.type == IT_FIXED && it.nullable) {
+                        const int vs = V.col_val[it.col];
+                        if (vs >= 0 && !vld[vs * VT + j]) { sz = 0; slack += it.size; }
+                    }
+                }
+            }
             pj[k] = (uint16_t)p;
             p += sz;
+            if (sz > 0xFFFFu) p = 0x10000u;  // forces the fallback below
         }
         pj[NI] = (uint16_t)p;
-        const uint32_t tot = p + (P.mode == PACKOS_MODE_PACKABLE ? slk[j] : 0u);
-        bsz[j] = tot;
+        const uint32_t tot = p + (P.mode == PACKOS_MODE_PACKABLE ? slack : 0u);
         if (p > 0xFFFFu || boff[j + 1] - boff[j] != tot || boff[j] + tot > cap) atomicOr(&misc[0], 1u);
     }
+    var_store(tid);
+    for (uint32_t c0 = tid + kVBatch * kBlock; c0 < vch; c0 += kVBatch * kBlock) {
+        var_load(c0);
+        var_store(c0);
+    }
     __syncthreads();
+    mark(1);
     if (misc[0]) {  // outside the tile plan: one wavefront per blob, straight to HBM
+        if (tid == 0) tflags[blockIdx.x] = 0u;
         uint32_t* wpos = (uint32_t*)obuf + wave * NP;
         for (uint32_t j = wave; j < rows; j += kWavesPerBlock)
             var_blob_wave(P, cols, lo + j, boff[j], out, cap, status, nullptr, wpos, lane);
         return;
     }
-    // R: runs of blobs whose start offsets share a kVWin window
-    if (wave == 0) {
-        const uint32_t win = (uint32_t)((boff[min((uint32_t)lane, rows - 1)] - boff[0]) / kVWin);
-        const uint32_t prev = __shfl_up(win, 1, kWave);
-        const bool isnew = (uint32_t)lane < rows && (lane == 0 || win != prev);
+    // ---- runs -----------------------------------------------------------------
+    {
+        const uint32_t j = tid;
+        const uint32_t win = j < rows ? (uint32_t)((boff[j] - boff[0]) >> win_shift) : 0u;
+        const uint32_t winp = (j > 0 && j < rows) ? (uint32_t)((boff[j - 1] - boff[0]) >> win_shift) : 0u;
+        const bool isnew = j < rows && (j == 0 || win != winp);
         const uint64_t bal = __ballot(isnew);
-        if (isnew) subs[__popcll(bal & ((1ull << lane) - 1ull))] = lane;
-        if (lane == 0) {
-            misc[1] = (uint32_t)__popcll(bal);
-            subs[__popcll(bal)] = rows;
+        if (lane == 0) misc[4 + wave] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t base = 0, tot = 0;
+        for (int w = 0; w < kWavesPerBlock; w++) {
+            base += w < wave ? misc[4 + w] : 0u;
+            tot += misc[4 + w];
+        }
+        if (isnew) subs[base + __popcll(bal & ((1ull << lane) - 1ull))] = j;
+        if (tid == 0) {
+            misc[1] = tot;
+            subs[tot] = rows;
         }
     }
     __syncthreads();
+    mark(2);
     const uint32_t nsub = misc[1];
     for (uint32_t q = 0; q < nsub; q++) {
         const uint32_t a = subs[q], b = subs[q + 1];
         const uint64_t s0 = boff[a], s1 = boff[b];
         const uint64_t al = s0 & ~15ull;
         const uint32_t nb = (uint32_t)(s1 - al);
-        if (nb + 16 > (uint32_t)kVBud) {
+        if (nb + 16 > bud) {
             uint32_t* wpos = (uint32_t*)obuf + wave * NP;
             for (uint32_t j = a + wave; j < b; j += kWavesPerBlock)
                 var_blob_wave(P, cols, lo + j, boff[j], out, cap, status, nullptr, wpos, lane);
-            for (uint32_t j = a + tid; j < b; j += kBlock) bst[j] = 2u;  // status already written
+            for (uint32_t j = a + tid; j < b; j += kBlock) bst[j] = 2u;  // status written, bytes complete
             __syncthreads();
             continue;
         }
         const uint32_t nch = (nb + 15) >> 4;
         for (uint32_t c = tid; c < nch; c += kBlock) ((u32x4*)obuf)[c] = u32x4{0u, 0u, 0u, 0u};
+        if (any_direct)
+            for (uint32_t c = tid; c < (nch + 31) / 32; c += kBlock) skip[c] = 0u;
         __syncthreads();
-        // header words
-        for (uint32_t t = tid; t < (b - a) * (uint32_t)NH; t += kBlock) {
-            const uint32_t jj = fast_div(t, (uint32_t)NH, nh_mag), hh = t - jj * (uint32_t)NH;
-            const uint32_t j = a + jj;
-            const EncHdr h = P.hdrs[hh];
+        const uint32_t nbr = b - a, nb_mag = magic_of(nbr);
+        // header words: (header, blob) pairs
+        for (uint32_t t = tid; t < nbr * (uint32_t)NH; t += kBlock) {
+            const uint32_t hh = fast_div(t, nbr, nb_mag), j = a + (t - hh * nbr);
+            const EncHdr h = hdrs[hh];
             if (!((pmk[j] >> h.cont) & 1ull)) continue;
             const uint16_t* pj = pos + j * NP;
             const uint32_t hpos = pj[h.hdr_item];
             uint16_t v;
             bool ovf;
             if (h.relative) {
-                const int64_t off = (int64_t)pj[h.target] - (int64_t)(hpos + P.items[h.hdr_item].size);
+                const int64_t off = (int64_t)pj[h.target] - (int64_t)(hpos + items[h.hdr_item].size);
                 ovf = off >= 8192;
                 v = enc_header(off, h.tag);
             } else {
@@ -760,58 +960,191 @@ __global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCol
             obuf[d] = (uint8_t)v;
             obuf[d + 1] = (uint8_t)(v >> 8);
         }
-        // items
-        for (int k = 0; k < NI; k++) {
-            const EncItem it = P.items[k];
+        // items: (item, blob) pairs, item-major
+        for (uint32_t t = tid; t < nbr * (uint32_t)NI; t += kBlock) {
+            const uint32_t k = fast_div(t, nbr, nb_mag), j = a + (t - k * nbr);
+            const EncItem it = items[k];
             if (it.type == IT_HDR) continue;
-            if (it.type != IT_VAR) {
-                const uint32_t w = it.size, mg = imag[k];
-                const bool lit = it.type == IT_CONST;
-                const uint8_t* src = lit ? P.lits + it.lit : cols.data[it.col] + (lo + a) * (uint64_t)w;
-                for (uint32_t t = tid; t < (b - a) * w; t += kBlock) {
-                    const uint32_t jj = fast_div(t, w, mg), bb = t - jj * w;
-                    const uint32_t j = a + jj;
-                    const uint16_t* pj = pos + j * NP;
-                    const uint32_t p0 = pj[k];
-                    if (pj[k + 1] == p0) continue;  // absent (nil leaf or container)
-                    uint32_t x = lit ? src[bb] : src[t];
-                    if (it.is_bool) x = x != 0;
-                    obuf[(uint32_t)(boff[j] - al) + p0 + bb] = (uint8_t)x;
-                }
+            const uint16_t* pj = pos + j * NP;
+            const uint32_t p0 = pj[k], len = (uint32_t)(pj[k + 1] - p0);
+            if (len == 0) continue;
+            uint8_t* d = obuf + (uint32_t)(boff[j] - al) + p0;
+            const uint8_t* sp;
+            if (it.type == IT_CONST) {
+                sp = lits + it.lit;
+            } else if (it.type == IT_FIXED) {
+                sp = stg + fmis[it.reg] + j * it.size;
             } else {
-                const uint32_t* vo = voff + ivs[k] * (kVT + 1);
-                const uint32_t v0 = vo[a], v1 = vo[b];
-                const uint8_t* src = cols.data[it.col];
-                for (uint32_t t = v0 + tid; t < v1; t += kBlock) {
-                    uint32_t l = a, r = b - 1;  // last blob j with vo[j] <= t
-                    while (l < r) {
-                        const uint32_t m = (l + r + 1) >> 1;
-                        if (vo[m] <= t) l = m; else r = m - 1;
-                    }
-                    const uint16_t* pj = pos + l * NP;
-                    const uint32_t p0 = pj[k], rel = t - vo[l];
-                    if (rel < (uint32_t)(pj[k + 1] - p0)) obuf[(uint32_t)(boff[l] - al) + p0 + rel] = src[t];
+                const VVar g = vvar[it.vslot];
+                if (g.lds_off == UINT32_MAX) {  // k_var_copy writes the value: mark its whole chunks
+                    const uint32_t rel = (uint32_t)(boff[j] - al) + p0;
+                    const uint32_t c0 = (rel + 15) >> 4, c1 = (rel + len) >> 4;
+                    for (uint32_t c = c0; c < c1; c++) atomicOr(&skip[c >> 5], 1u << (c & 31));
+                    continue;
                 }
+                sp = stg + g.lds_off + (uint32_t)(g.src & 15) + (voff[it.vslot * (VT + 1) + j] - voff[it.vslot * (VT + 1)]);
+            }
+            if (it.is_bool) {
+                d[0] = sp[0] != 0;
+            } else {
+#pragma unroll 4
+                for (uint32_t x = 0; x < len; x++) d[x] = sp[x];
             }
         }
         __syncthreads();
         // write [s0, s1)
         for (uint32_t c = tid; c < nch; c += kBlock) {
             const uint64_t g0 = al + 16ull * c;
+            if (any_direct && ((skip[c >> 5] >> (c & 31)) & 1u)) continue;
             if (g0 >= s0 && g0 + 16 <= s1) {
                 __builtin_nontemporal_store(((const u32x4*)obuf)[c], (u32x4*)(out + g0));
             } else {
                 for (int x = 0; x < 16; x++) {
-                    const uint64_t g = g0 + x;
-                    if (g >= s0 && g < s1) out[g] = obuf[16 * c + x];
+                    const uint64_t gg = g0 + x;
+                    if (gg >= s0 && gg < s1) out[gg] = obuf[16 * c + x];
                 }
             }
         }
         __syncthreads();
     }
+    mark(3);
+    // ---- unstaged var values: hand their positions to k_var_copy -------------
+    if (tid == 0) {
+        uint32_t fl = 0;
+        for (int vv = 0; vv < V.nvar; vv++) fl |= (vvar[vv].lds_off == UINT32_MAX ? 1u : 0u) << vv;
+        tflags[blockIdx.x] = fl;
+    }
+    if (any_direct) {
+        for (int vv = 0; vv < V.nvar; vv++) {
+            if (vvar[vv].lds_off != UINT32_MAX) continue;
+            const int k = V.var_item[vv];
+            for (uint32_t j = tid; j < rows; j += kBlock)
+                vpos[(uint64_t)vv * n + lo + j] = (bst[j] & 2u) ? (uint16_t)0xFFFFu : pos[j * NP + k];
+        }
+    }
+    mark(4);
     if (status)
         for (uint32_t j = tid; j < rows; j += kBlock)
             if (!(bst[j] & 2u)) status[lo + j] = (bst[j] & 1u) ? PACKOS_STATUS_OVERFLOW13 : 0u;
+}
+
+// Long var values the tile kernel did not stage: a flattened memmove per
+// tile over 16-B-aligned destination chunks, consecutive lanes on
+// consecutive chunks.  A chunk wholly inside one value takes two aligned 16-B
+// source loads, a funnel shift and one 16-B store; the (at most two) edge
+// chunks of a value go byte by byte.  Runs after k_encode_var_tile, which
+// skipped the whole chunks and wrote the edge chunks' other bytes.
+constexpr int kCopyBatch = 4;
+
+__device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return q == 0 ? a : q == 1 ? b : q == 2 ? c : d;
+}
+
+template <int VT>
+__global__ __launch_bounds__(kBlock) void k_var_copy(VarPlan V, const uint64_t* __restrict__ offs,
+                                                     const uint32_t* __restrict__ tflags,
+                                                     const uint16_t* __restrict__ vpos, uint8_t* __restrict__ out,
+                                                     uint64_t n) {
+    __shared__ uint64_t boff[VT + 1];
+    __shared__ uint32_t vo[VT + 1], uo[VT + 1];
+    __shared__ uint16_t ps[VT];
+    __shared__ uint32_t wsum[kWavesPerBlock];
+    const uint32_t fl = tflags[blockIdx.x];
+    if (!fl) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t lo = (uint64_t)blockIdx.x * VT;
+    const uint32_t rows = (uint32_t)min((uint64_t)VT, n - lo);
+    for (uint32_t j = tid; j <= rows; j += kBlock) boff[j] = offs[lo + j];
+    for (int v = 0; v < V.nvar; v++) {
+        if (!((fl >> v) & 1u)) continue;
+        const uint32_t* voff_g = V.var_off[v];
+        for (uint32_t j = tid; j <= rows; j += kBlock) vo[j] = voff_g[lo + j];
+        for (uint32_t j = tid; j < rows; j += kBlock) ps[j] = vpos[(uint64_t)v * n + lo + j];
+        __syncthreads();
+        {
+            const uint32_t j = tid;
+            uint32_t cnt = 0;
+            if (j < rows && ps[j] != 0xFFFFu) {
+                const uint64_t d0 = boff[j] + ps[j];
+                const uint32_t len = vo[j + 1] - vo[j];
+                cnt = len ? (uint32_t)(((d0 + len + 15) >> 4) - (d0 >> 4)) : 0u;
+            }
+            const uint32_t incl = wave_incl_scan(cnt, lane);
+            if (lane == 63) wsum[wave] = incl;
+            __syncthreads();
+            uint32_t wb = 0, tot = 0;
+            for (int w = 0; w < kWavesPerBlock; w++) {
+                wb += w < wave ? wsum[w] : 0u;
+                tot += wsum[w];
+            }
+            if (j < rows) uo[j] = wb + incl - cnt;
+            if (tid == 0) uo[rows] = tot;
+            __syncthreads();
+        }
+        const uint32_t U = uo[rows];
+        const uint8_t* col = V.var_data[v];
+        for (uint32_t u0 = tid; u0 < U; u0 += kCopyBatch * kBlock) {
+            u32x4 a[kCopyBatch], b[kCopyBatch];
+            uint64_t dst[kCopyBatch], d0s[kCopyBatch];
+            uint32_t sh[kCopyBatch], jj[kCopyBatch], len[kCopyBatch];
+            bool full[kCopyBatch];
+#pragma unroll
+            for (int m = 0; m < kCopyBatch; m++) {
+                const uint32_t u = u0 + m * kBlock;
+                full[m] = false;
+                if (u >= U) continue;
+                uint32_t l = 0, r = rows - 1;  // last blob j with uo[j] <= u
+                while (l < r) {
+                    const uint32_t mm = (l + r + 1) >> 1;
+                    if (uo[mm] <= u) l = mm; else r = mm - 1;
+                }
+                const uint64_t d0 = boff[l] + ps[l];
+                const uint32_t ln = vo[l + 1] - vo[l];
+                const uint64_t C = (d0 >> 4) + (u - uo[l]);
+                jj[m] = l;
+                d0s[m] = d0;
+                len[m] = ln;
+                dst[m] = 16 * C;
+                full[m] = 16 * C >= d0 && 16 * C + 16 <= d0 + ln;
+                if (full[m]) {
+                    const uintptr_t xa = (uintptr_t)(col + vo[l] + (16 * C - d0));
+                    const g_u32x4* xw = (const g_u32x4*)(xa & ~(uintptr_t)15);
+                    sh[m] = (uint32_t)(xa & 15);
+                    a[m] = xw[0];
+                    if (sh[m]) b[m] = xw[1];
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < kCopyBatch; m++) {
+                const uint32_t u = u0 + m * kBlock;
+                if (u >= U) continue;
+                if (full[m]) {
+                    u32x4 o4;
+                    if (sh[m] == 0) {
+                        o4 = a[m];
+                    } else {
+                        const uint32_t q = sh[m] >> 2, s = sh[m] & 3;
+                        const uint32_t w[8] = {a[m].x, a[m].y, a[m].z, a[m].w, b[m].x, b[m].y, b[m].z, b[m].w};
+                        uint32_t t5[5];
+#pragma unroll
+                        for (int i = 0; i < 5; i++) t5[i] = sel4(q, w[i], w[i + 1], w[i + 2], w[i + 3]);
+                        o4.x = s ? __builtin_amdgcn_alignbyte(t5[1], t5[0], s) : t5[0];
+                        o4.y = s ? __builtin_amdgcn_alignbyte(t5[2], t5[1], s) : t5[1];
+                        o4.z = s ? __builtin_amdgcn_alignbyte(t5[3], t5[2], s) : t5[2];
+                        o4.w = s ? __builtin_amdgcn_alignbyte(t5[4], t5[3], s) : t5[3];
+                    }
+                    __builtin_nontemporal_store(o4, (u32x4*)(out + dst[m]));
+                } else {
+                    const uint64_t d0 = d0s[m];
+                    const uint64_t g0 = dst[m] > d0 ? dst[m] : d0;
+                    const uint64_t g1 = min(dst[m] + 16, d0 + len[m]);
+                    const uint8_t* sp = col + vo[jj[m]];
+                    for (uint64_t g = g0; g < g1; g++) out[g] = sp[g - d0];
+                }
+            }
+        }
+        __syncthreads();
+    }
 }
 
 // =========================================================================
@@ -1305,6 +1638,7 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     t.enc.n_hdrs = (int)s->hdrs.size();
     t.enc.n_conts = (int)s->conts.size();
     t.enc.mode = s->mode;
+    t.enc.n_lits = (int)s->lits.size();
     t.fix.segs = (const FixSeg*)(b + o_fsegs);
     t.fix.seg_index = (const uint32_t*)(b + o_fidx);
     t.fix.fcols = (const FixCol*)(b + o_fcols);
@@ -1353,10 +1687,17 @@ void packos_schema_free(packos_schema* s) {
     delete s;
 }
 
+// [scan tile sums][tile flags (k_var_copy)][value positions (u16, per var leaf x blob)]
+static size_t ws_scan_bytes(size_t n) { return (((n + kScanTile - 1) / kScanTile) + 16) * sizeof(uint64_t); }
+static size_t ws_flag_bytes(size_t n) { return ((n + 63) / 64 + 4) * sizeof(uint32_t); }
+
 size_t packos_encode_workspace_size(const packos_schema* s, size_t n_blobs) {
-    (void)s;
-    size_t nb = (n_blobs + kScanTile - 1) / kScanTile;
-    return (nb + 16) * sizeof(uint64_t);
+    size_t nvar = 0;
+    if (s)
+        for (const EncItem& it : s->items) nvar += it.type == IT_VAR;
+    const size_t a = (ws_scan_bytes(n_blobs) + 255) & ~(size_t)255;
+    const size_t b = (ws_flag_bytes(n_blobs) + 255) & ~(size_t)255;
+    return a + b + nvar * n_blobs * sizeof(uint16_t) + 256;
 }
 
 static int size_pass(packos_schema* s, DeviceTables* t, const EncCols& ec, size_t n, uint64_t* offs, void* ws,
@@ -1488,15 +1829,93 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
         return PACKOS_E_INVALID;
     }
     const size_t npos = s->items.size() + 1;
-    int nvar = 0;
-    for (const EncItem& it : s->items) nvar += it.type == IT_VAR;
-    const VtLayout vl = vt_layout((int)s->items.size(), nvar);
-    const bool tiled = !(flags & PACKOS_ENC_FORCE_GENERIC) && vl.total <= 64 * 1024 && nvar < 256 &&
-                       npos * 4 * kWavesPerBlock <= (size_t)kVBud;
+    int vt = 128;
+    uint32_t bud = 16384, in_bud = 16384;
+    if (const char* e = getenv("PACKOS_VAR_TILE")) vt = atoi(e);
+    if (const char* e = getenv("PACKOS_VAR_BUD")) bud = (uint32_t)std::max(2048, std::min(32768, atoi(e)));
+    if (const char* e = getenv("PACKOS_VAR_IN")) in_bud = (uint32_t)std::max(0, std::min(32768, atoi(e)));
+    if (vt != 64 && vt != 256) vt = 128;
+    uint32_t win_shift = 0;
+    while ((2u << win_shift) <= bud / 2) win_shift++;
+    // per-call plan: fixed regions (IT_FIXED items), var leaves, validity columns
+    VarPlan vp;
+    memset(&vp, 0, sizeof(vp));
+    for (int c = 0; c < kMaxCols; c++) vp.col_val[c] = -1;
+    bool plan_ok = !(flags & PACKOS_ENC_FORCE_GENERIC) && s->conts.size() <= 64 && s->items.size() < 255;
+    for (size_t c = 0; c < s->col_node.size() && plan_ok; c++) {
+        if (!ec.valid[c]) continue;
+        if (vp.nval >= kVPVal) { plan_ok = false; break; }
+        vp.col_val[c] = (int8_t)vp.nval;
+        vp.val_ptr[vp.nval++] = ec.valid[c];
+    }
+    auto plan_for = [&](int tile) {
+        vp.nfix = vp.nvar = 0;
+        uint32_t fb = 0;
+        for (size_t k = 0; k < s->items.size() && plan_ok; k++) {
+            const EncItem& it = s->items[k];
+            if (it.type == IT_FIXED) {
+                if (vp.nfix >= kVPFix) { plan_ok = false; break; }
+                vp.fix_ptr[vp.nfix] = ec.data[it.col];
+                vp.fix_w[vp.nfix] = it.size;
+                vp.fix_lds[vp.nfix] = fb;
+                fb += ((uint32_t)tile * it.size + 16 + 15) & ~15u;
+                vp.nfix++;
+            } else if (it.type == IT_VAR) {
+                if (vp.nvar >= kVPVar) { plan_ok = false; break; }
+                vp.var_off[vp.nvar] = ec.off[it.col];
+                vp.var_data[vp.nvar] = ec.data[it.col];
+                vp.var_item[vp.nvar] = (int)k;
+                vp.nvar++;
+            }
+        }
+        vp.fix_bytes = (int32_t)fb;
+        return fb;
+    };
+    VtLayout vl{};
+    uint32_t fb = 0;
+    for (;;) {
+        fb = plan_for(vt);
+        const uint32_t ib = std::max(in_bud, fb);  // fixed regions are always staged
+        vl = vt_layout(vt, t->enc, vp.nvar, vp.nval, bud, ib);
+        if ((vl.total <= 64 * 1024 && fb <= 32768) || vt == 64) break;
+        vt /= 2;
+    }
+    in_bud = std::max(in_bud, fb);
+    const bool tiled = plan_ok && vl.total <= 64 * 1024 && npos * 4 * kWavesPerBlock <= (size_t)bud &&
+                       ws && ws_bytes >= packos_encode_workspace_size(s, n);
     if (tiled) {
-        hipLaunchKernelGGL(k_encode_var_tile, dim3((unsigned)((n + kVT - 1) / kVT)), dim3(kBlock), (size_t)vl.total,
-                           st, t->enc, ec, (const uint64_t*)out_offsets, out, cap, (uint64_t)n, status, nvar);
+        uint8_t* wsb = (uint8_t*)ws + ((ws_scan_bytes(n) + 255) & ~(size_t)255);
+        uint32_t* tflags = (uint32_t*)wsb;
+        uint16_t* vpos = (uint16_t*)(wsb + ((ws_flag_bytes(n) + 255) & ~(size_t)255));
+        const dim3 g((unsigned)((n + vt - 1) / vt)), b(kBlock);
+        const size_t l = vl.total;
+        const uint64_t* o = out_offsets;
+        static unsigned long long* prof = nullptr;  // debug: PACKOS_VAR_PROF=1 prints phase cycles
+        const bool want_prof = getenv("PACKOS_VAR_PROF") != nullptr;
+        if (want_prof && !prof) HIP_TRY(hipMalloc(&prof, 16 * sizeof(unsigned long long)));
+        if (want_prof) HIP_TRY(hipMemsetAsync(prof, 0, 16 * sizeof(unsigned long long), st));
+        unsigned long long* pp = want_prof ? prof : nullptr;
+        if (vt == 64)
+            hipLaunchKernelGGL(k_encode_var_tile<64>, g, b, l, st, t->enc, ec, vp, o, out, cap, (uint64_t)n, status, bud, win_shift, in_bud, tflags, vpos, pp);
+        else if (vt == 128)
+            hipLaunchKernelGGL(k_encode_var_tile<128>, g, b, l, st, t->enc, ec, vp, o, out, cap, (uint64_t)n, status, bud, win_shift, in_bud, tflags, vpos, pp);
+        else
+            hipLaunchKernelGGL(k_encode_var_tile<256>, g, b, l, st, t->enc, ec, vp, o, out, cap, (uint64_t)n, status, bud, win_shift, in_bud, tflags, vpos, pp);
         HIP_TRY(hipGetLastError());
+        if (vp.nvar > 0) {
+            if (vt == 64) hipLaunchKernelGGL(k_var_copy<64>, g, b, 0, st, vp, o, tflags, vpos, out, (uint64_t)n);
+            else if (vt == 128) hipLaunchKernelGGL(k_var_copy<128>, g, b, 0, st, vp, o, tflags, vpos, out, (uint64_t)n);
+            else hipLaunchKernelGGL(k_var_copy<256>, g, b, 0, st, vp, o, tflags, vpos, out, (uint64_t)n);
+            HIP_TRY(hipGetLastError());
+        }
+        if (want_prof) {
+            unsigned long long h[16];
+            HIP_TRY(hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            fprintf(stderr, "var_tile vt=%d lds=%zu blocks=%u ticks/block:", vt, l, g.x);
+            for (int i = 0; i < 5; i++) fprintf(stderr, " p%d=%.0f", i, (double)h[i] / g.x);
+            fprintf(stderr, "\n");
+        }
         return PACKOS_OK;
     }
     const size_t lds = (size_t)kWavesPerBlock * (kSlot + ((npos * 4 + 15) / 16) * 16);

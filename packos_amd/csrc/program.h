@@ -25,11 +25,14 @@ struct EncItem {
     uint8_t type;      // IT_*
     uint8_t nullable;  // fixed leaf with a validity column
     uint8_t is_bool;   // normalise any non-zero input byte to 1
-    uint8_t pad;
+    uint8_t vslot;     // IT_VAR: index among the var items
     int16_t cont;      // container whose presence gates this item
     int16_t col;       // leaf column (IT_FIXED / IT_VAR), -1 otherwise
     uint32_t size;     // fixed width / literal length / header-block bytes
     uint32_t lit;      // literal offset (IT_CONST)
+    uint32_t magic;    // ceil(2^32 / size) when size > 1 (division by size)
+    uint8_t reg;       // IT_FIXED: index among the fixed items (staging region), 255 otherwise
+    uint8_t pad[3];
 };
 
 struct EncHdr {            // one uint16 header word
@@ -57,6 +60,7 @@ struct EncProgram {
     const EncCont* conts;
     const uint8_t* lits;
     int32_t n_items, n_hdrs, n_conts, mode;
+    int32_t n_lits;
 };
 
 // Fixed-size layout (no var-width leaves, no nils in the call): every blob is
