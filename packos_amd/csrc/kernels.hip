@@ -979,7 +979,11 @@ __global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCol
                 if (g.lds_off == UINT32_MAX) {  // k_var_copy writes the value: mark its whole chunks
                     const uint32_t rel = (uint32_t)(boff[j] - al) + p0;
                     const uint32_t c0 = (rel + 15) >> 4, c1 = (rel + len) >> 4;
-                    for (uint32_t c = c0; c < c1; c++) atomicOr(&skip[c >> 5], 1u << (c & 31));
+                    for (uint32_t w = c0 >> 5; c0 < c1 && w <= (c1 - 1) >> 5; w++) {
+                        const uint32_t b0 = max(c0, w * 32) - w * 32, b1 = min(c1, w * 32 + 32) - w * 32;
+                        const uint32_t mask = (b1 - b0 == 32) ? ~0u : (((1u << (b1 - b0)) - 1u) << b0);
+                        atomicOr(&skip[w], mask);
+                    }
                     continue;
                 }
                 sp = stg + g.lds_off + (uint32_t)(g.src & 15) + (voff[it.vslot * (VT + 1) + j] - voff[it.vslot * (VT + 1)]);
@@ -1085,13 +1089,15 @@ __global__ __launch_bounds__(kBlock) void k_var_copy(VarPlan V, const uint64_t* 
         const uint8_t* col = V.var_data[v];
         for (uint32_t u0 = tid; u0 < U; u0 += kCopyBatch * kBlock) {
             u32x4 a[kCopyBatch], b[kCopyBatch];
-            uint64_t dst[kCopyBatch], d0s[kCopyBatch];
-            uint32_t sh[kCopyBatch], jj[kCopyBatch], len[kCopyBatch];
-            bool full[kCopyBatch];
+            uint64_t dst[kCopyBatch];
+            uint32_t sh[kCopyBatch], k0[kCopyBatch], k1[kCopyBatch];
 #pragma unroll
             for (int m = 0; m < kCopyBatch; m++) {
                 const uint32_t u = u0 + m * kBlock;
-                full[m] = false;
+                k0[m] = k1[m] = 0;
+                sh[m] = 0;
+                dst[m] = 0;
+                a[m] = b[m] = u32x4{0u, 0u, 0u, 0u};
                 if (u >= U) continue;
                 uint32_t l = 0, r = rows - 1;  // last blob j with uo[j] <= u
                 while (l < r) {
@@ -1100,46 +1106,43 @@ __global__ __launch_bounds__(kBlock) void k_var_copy(VarPlan V, const uint64_t* 
                 }
                 const uint64_t d0 = boff[l] + ps[l];
                 const uint32_t ln = vo[l + 1] - vo[l];
-                const uint64_t C = (d0 >> 4) + (u - uo[l]);
-                jj[m] = l;
-                d0s[m] = d0;
-                len[m] = ln;
-                dst[m] = 16 * C;
-                full[m] = 16 * C >= d0 && 16 * C + 16 <= d0 + ln;
-                if (full[m]) {
-                    const uintptr_t xa = (uintptr_t)(col + vo[l] + (16 * C - d0));
-                    const g_u32x4* xw = (const g_u32x4*)(xa & ~(uintptr_t)15);
-                    sh[m] = (uint32_t)(xa & 15);
-                    a[m] = xw[0];
-                    if (sh[m]) b[m] = xw[1];
-                }
+                const uint64_t C = 16 * ((d0 >> 4) + (u - uo[l]));
+                dst[m] = C;
+                // chunk bytes [k0, k1) belong to the value
+                k0[m] = C >= d0 ? 0u : (uint32_t)(d0 - C);
+                k1[m] = (uint32_t)min((uint64_t)16, d0 + ln - C);
+                // source of chunk byte 0 (may lie outside the value for an edge chunk:
+                // only the aligned blocks that hold needed bytes are read)
+                const uintptr_t xa = (uintptr_t)(col + vo[l]) + (uintptr_t)(C - d0);
+                const g_u32x4* xw = (const g_u32x4*)(xa & ~(uintptr_t)15);
+                sh[m] = (uint32_t)(xa & 15);
+                if (k0[m] < 16 - sh[m]) a[m] = xw[0];
+                if (sh[m] && k1[m] > 16 - sh[m]) b[m] = xw[1];
             }
 #pragma unroll
             for (int m = 0; m < kCopyBatch; m++) {
-                const uint32_t u = u0 + m * kBlock;
-                if (u >= U) continue;
-                if (full[m]) {
-                    u32x4 o4;
-                    if (sh[m] == 0) {
-                        o4 = a[m];
-                    } else {
-                        const uint32_t q = sh[m] >> 2, s = sh[m] & 3;
-                        const uint32_t w[8] = {a[m].x, a[m].y, a[m].z, a[m].w, b[m].x, b[m].y, b[m].z, b[m].w};
-                        uint32_t t5[5];
+                if (u0 + m * kBlock >= U) continue;
+                u32x4 o4;
+                if (sh[m] == 0) {
+                    o4 = a[m];
+                } else {
+                    const uint32_t q = sh[m] >> 2, sb = sh[m] & 3;
+                    const uint32_t w[8] = {a[m].x, a[m].y, a[m].z, a[m].w, b[m].x, b[m].y, b[m].z, b[m].w};
+                    uint32_t t5[5];
 #pragma unroll
-                        for (int i = 0; i < 5; i++) t5[i] = sel4(q, w[i], w[i + 1], w[i + 2], w[i + 3]);
-                        o4.x = s ? __builtin_amdgcn_alignbyte(t5[1], t5[0], s) : t5[0];
-                        o4.y = s ? __builtin_amdgcn_alignbyte(t5[2], t5[1], s) : t5[1];
-                        o4.z = s ? __builtin_amdgcn_alignbyte(t5[3], t5[2], s) : t5[2];
-                        o4.w = s ? __builtin_amdgcn_alignbyte(t5[4], t5[3], s) : t5[3];
-                    }
+                    for (int i = 0; i < 5; i++) t5[i] = sel4(q, w[i], w[i + 1], w[i + 2], w[i + 3]);
+                    o4.x = sb ? __builtin_amdgcn_alignbyte(t5[1], t5[0], sb) : t5[0];
+                    o4.y = sb ? __builtin_amdgcn_alignbyte(t5[2], t5[1], sb) : t5[1];
+                    o4.z = sb ? __builtin_amdgcn_alignbyte(t5[3], t5[2], sb) : t5[2];
+                    o4.w = sb ? __builtin_amdgcn_alignbyte(t5[4], t5[3], sb) : t5[3];
+                }
+                if (k0[m] == 0 && k1[m] == 16) {
                     __builtin_nontemporal_store(o4, (u32x4*)(out + dst[m]));
                 } else {
-                    const uint64_t d0 = d0s[m];
-                    const uint64_t g0 = dst[m] > d0 ? dst[m] : d0;
-                    const uint64_t g1 = min(dst[m] + 16, d0 + len[m]);
-                    const uint8_t* sp = col + vo[jj[m]];
-                    for (uint64_t g = g0; g < g1; g++) out[g] = sp[g - d0];
+                    const uint32_t wv[4] = {o4.x, o4.y, o4.z, o4.w};
+#pragma unroll
+                    for (int x = 0; x < 16; x++)
+                        if ((uint32_t)x >= k0[m] && (uint32_t)x < k1[m]) out[dst[m] + x] = (uint8_t)(wv[x >> 2] >> (8 * (x & 3)));
                 }
             }
         }
@@ -1160,27 +1163,48 @@ struct DSeq {
 
 __host__ __device__ __forceinline__ uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
 
+// Byte readers for the decoder: straight from the arena, or from a per-blob
+// LDS window (the blob's first W bytes) with the arena behind it.
+struct GReader {
+    const uint8_t* a;
+    __host__ __device__ __forceinline__ uint32_t operator()(uint64_t p) const { return a[p]; }
+};
+struct WReader {
+    const uint8_t* a;
+    const uint8_t* win;   // LDS copy of arena[base, base + W)
+    uint64_t base;
+    uint32_t W;
+    __device__ __forceinline__ uint32_t operator()(uint64_t p) const {
+        const uint64_t d = p - base;
+        return d < W ? win[d] : a[p];
+    }
+};
+template <class R>
+__host__ __device__ __forceinline__ uint16_t rd16r(const R& r, uint64_t p) { return (uint16_t)(r(p) | (r(p + 1) << 8)); }
+
 // NewSeqGetAccess (seqget.go:22-47)
-__host__ __device__ __forceinline__ int dseq_init(DSeq& s, const uint8_t* a, uint64_t start, int64_t len) {
+template <class R>
+__host__ __device__ __forceinline__ int dseq_init(DSeq& s, const R& a, uint64_t start, int64_t len) {
     if (len < 4) return 1;
-    const uint16_t h0 = rd16(a + start);
+    const uint16_t h0 = rd16r(a, start);
     const int64_t base = h0 >> 3;
     if (len < base) return 1;
-    const uint16_t h1 = rd16(a + start + 2);
+    const uint16_t h1 = rd16r(a, start + 2);
     s.len = len; s.base = base; s.count = base / 2; s.pos = 0; s.start = start;
     s.cur_off = base; s.cur_type = h0 & 7;
     s.next_off = (h1 >> 3) + base; s.next_type = h1 & 7;
     return 0;
 }
 // Advance (seqget.go:85-103): 0 ok, 1 out of bounds, 2 Go panic (unchecked header read)
-__host__ __device__ __forceinline__ int dseq_advance(DSeq& s, const uint8_t* a) {
+template <class R>
+__host__ __device__ __forceinline__ int dseq_advance(DSeq& s, const R& a) {
     if (s.pos + 2 > s.count) return 1;
     s.pos++;
     s.cur_off = s.next_off;
     s.cur_type = s.next_type;
     if (s.cur_type != 0) {
         if ((s.pos + 1) * 2 + 2 > s.len) return 2;
-        const uint16_t h = rd16(a + s.start + (s.pos + 1) * 2);
+        const uint16_t h = rd16r(a, s.start + (s.pos + 1) * 2);
         s.next_off = (h >> 3) + s.base;
         s.next_type = h & 7;
     }
@@ -1198,6 +1222,17 @@ __host__ __device__ __forceinline__ int dprecheck(const DSeq& s, int tag, int64_
 
 constexpr int kPanic = 0x100;
 
+// w bytes from reader position p to a column row; dword stores when aligned
+template <class R>
+__host__ __device__ __forceinline__ void copy_out(uint8_t* dst, const R& r, uint64_t p, uint32_t w) {
+    if ((w & 3) == 0 && ((uintptr_t)dst & 3) == 0) {
+        for (uint32_t j = 0; j < w; j += 4)
+            *(uint32_t*)(dst + j) = r(p + j) | (r(p + j + 1) << 8) | (r(p + j + 2) << 16) | (r(p + j + 3) << 24);
+    } else {
+        for (uint32_t j = 0; j < w; j++) dst[j] = (uint8_t)r(p + j);
+    }
+}
+
 struct Frame {
     DSeq q;
     int node;
@@ -1208,34 +1243,35 @@ struct Frame {
 // leaves into the output columns and returns the packed status word.  Host +
 // device: the host runs it once on the canonical blob to qualify a schema for
 // the fixed-layout fast path (same code, so the qualification is exact).
-__host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& cols, const uint8_t* arena, uint64_t a0,
+template <class R>
+__host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& cols, const R& arena, uint64_t a0,
                                          uint64_t a1, uint64_t i) {
-    Frame st[kDecDepth];
+    // the current frame lives in registers; outer frames are spilled to `stk`
+    // (scratch) only while a nested tuple/map is being read
+    Frame cur;
+    Frame stk[kDecDepth];
     int d = 0;
-    if (dseq_init(st[0].q, arena, a0, (int64_t)(a1 - a0)))
+    if (dseq_init(cur.q, arena, a0, (int64_t)(a1 - a0)))
         return (uint32_t)PACKOS_ERR_INVALID_FORMAT;  // position -1
-    st[0].node = P.root;
-    st[0].k = 0;
+    cur.node = P.root;
+    cur.k = 0;
     int err = 0;
     for (;;) {
-        Frame& f = st[d];
-        const DecNode fn = P.nodes[f.node];
-        if (f.k >= fn.nkids) {
+        const DecNode fn = P.nodes[cur.node];
+        if (cur.k >= fn.nkids) {
             if (d == 0) break;
             // container finished: mark it present, then Advance the parent past it
-            {
-                const DecNode cn = P.nodes[f.node];
-                if (cols.valid[cn.col]) cols.valid[cn.col][i] = 1;
-            }
+            if (cols.valid[fn.col]) cols.valid[fn.col][i] = 1;
             d--;
-            const int a = dseq_advance(st[d].q, arena);
+            cur = stk[d];
+            const int a = dseq_advance(cur.q, arena);
             if (a) { err = a == 2 ? kPanic : 2; break; }
-            st[d].k++;
+            cur.k++;
             continue;
         }
-        const int nid = P.kids[fn.kid0 + f.k];
+        const int nid = P.kids[fn.kid0 + cur.k];
         const DecNode nd = P.nodes[nid];
-        DSeq& q = f.q;
+        DSeq& q = cur.q;
         int64_t w = 0;
         if (nd.kind == K_TUPLE || nd.kind == K_MAP) {
             err = dprecheck(q, nd.tag, -1, nd.nullable, w);
@@ -1245,7 +1281,7 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
                 // PeekNestedSeq (seqget.go:105-121)
                 if (q.next_off - q.cur_off <= 0 || q.next_off > q.len) { err = 1; break; }
                 if (d + 1 >= kDecDepth) { err = 1; break; }
-                Frame& c = st[d + 1];
+                Frame c;
                 if (dseq_init(c.q, arena, q.start + q.cur_off, q.next_off - q.cur_off)) { err = 1; break; }
                 if (nd.kind == K_TUPLE && nd.nkids > 0 && (c.q.count - 1) != nd.nkids && !nd.variable) {
                     err = 3;
@@ -1253,13 +1289,15 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
                 }
                 c.node = nid;
                 c.k = 0;
+                stk[d] = cur;
+                cur = c;
                 d++;
                 continue;
             }
             if (cols.valid[nd.col]) cols.valid[nd.col][i] = 0;  // nil container
             const int a = dseq_advance(q, arena);
             if (a) { err = a == 2 ? kPanic : 2; break; }
-            f.k++;
+            cur.k++;
             continue;
         }
         // primitives: validatePrimitiveAndGetPayload (schema.go:1031-1052)
@@ -1271,7 +1309,7 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
             const int a = dseq_advance(q, arena);
             if (a) { err = a == 2 ? kPanic : 2; break; }
         }
-        const uint8_t* pay = arena + q.start + (ps < 0 ? 0 : ps);
+        const uint64_t pay = q.start + (ps < 0 ? 0 : ps);
         switch (nd.kind) {
             case K_INT: case K_UINT: case K_FLOAT: case K_BOOL: {
                 if (ps < 0) {
@@ -1280,15 +1318,15 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
                 }
                 if (w < nd.width) { err = kPanic; break; }  // LittleEndian.UintXX on a short slice
                 uint8_t* dstp = cols.data[nd.col] + i * (uint64_t)nd.width;
-                if (nd.kind == K_BOOL) dstp[0] = pay[0] != 0;
-                else for (int j = 0; j < nd.width; j++) dstp[j] = pay[j];
+                if (nd.kind == K_BOOL) dstp[0] = arena(pay) != 0;
+                else copy_out(dstp, arena, pay, (uint32_t)nd.width);
                 if (cols.valid[nd.col]) cols.valid[nd.col][i] = 1;
                 break;
             }
             case K_STRING: case K_BYTES:
                 if (nd.width > 0) {
                     uint8_t* dstp = cols.data[nd.col] + i * (uint64_t)nd.width;
-                    for (int j = 0; j < nd.width; j++) dstp[j] = pay[j];
+                    copy_out(dstp, arena, pay, (uint32_t)nd.width);
                 } else {
                     cols.start[nd.col][i] = ps < 0 ? 0ull : q.start + (uint64_t)ps;
                     cols.length[nd.col][i] = ps < 0 ? 0u : (uint32_t)w;
@@ -1297,17 +1335,17 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
             case K_MATCH: {
                 const uint32_t have = ps < 0 ? 0u : (uint32_t)w;
                 bool eq = have == nd.lit_len;
-                for (uint32_t j = 0; eq && j < have; j++) eq = pay[j] == P.lits[nd.lit + j];
+                for (uint32_t j = 0; eq && j < have; j++) eq = arena(pay + j) == P.lits[nd.lit + j];
                 if (!eq) err = PACKOS_ERR_STRING_MATCH;
                 break;
             }
         }
         if (err) break;
-        f.k++;
+        cur.k++;
     }
     uint32_t sv = 0;
     if (err) {
-        const uint32_t posv = (uint32_t)(st[0].k + 1) << 8;
+        const uint32_t posv = (uint32_t)((d == 0 ? cur.k : stk[0].k) + 1) << 8;
         if (err == kPanic) sv = PACKOS_STATUS_PANIC | posv;
         else sv = (uint32_t)(d == 0 ? err : PACKOS_ERR_INVALID_FORMAT) | posv;
     }
@@ -1322,7 +1360,41 @@ __global__ __launch_bounds__(kBlock) void k_decode(DecProgram P, DecCols cols, c
     if (i >= n) return;
     const uint64_t a0 = offs ? offs[i] : i * stride;
     const uint64_t a1 = offs ? offs[i + 1] : (i + 1) * stride;
-    status[i] = decode_blob(P, cols, arena, a0, a1, i);
+    status[i] = decode_blob(P, cols, GReader{arena}, a0, a1, i);
+}
+
+// Generic decode with a per-blob LDS window: every thread first fetches its
+// blob's first kDecWinChunks x 16 bytes (header block, leading fields) with
+// 16-B loads, all in flight, then runs decode_blob reading the window and
+// falling back to HBM only beyond it.  Replaces ~one dependent global byte
+// load per header word / payload byte with one load round.
+constexpr int kDecWinChunks = 8;
+
+__global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols cols, const uint8_t* __restrict__ arena,
+                                                       const uint64_t* __restrict__ offs, uint64_t stride, uint64_t n,
+                                                       uint32_t* __restrict__ status) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[kBlock * kDecWinChunks * 16];
+    const int tid = threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + tid;
+    uint64_t a0 = 0, a1 = 0;
+    if (i < n) {
+        a0 = offs ? offs[i] : i * stride;
+        a1 = offs ? offs[i + 1] : (i + 1) * stride;
+    }
+    uint8_t* w = win + tid * kDecWinChunks * 16;
+    const uint64_t b0 = a0 & ~15ull;
+    const uint64_t end = min(a1, b0 + 16ull * kDecWinChunks);
+    const uint32_t nch = (i < n && end > a0) ? (uint32_t)((end - b0 + 15) >> 4) : 0u;
+    u32x4 v[kDecWinChunks];
+#pragma unroll
+    for (int c = 0; c < kDecWinChunks; c++)
+        if ((uint32_t)c < nch) v[c] = *(const g_u32x4*)(arena + b0 + 16 * c);
+#pragma unroll
+    for (int c = 0; c < kDecWinChunks; c++)
+        if ((uint32_t)c < nch) *(u32x4*)(w + 16 * c) = v[c];
+    if (i >= n) return;
+    const WReader R{arena, w, b0, 16 * nch};
+    status[i] = decode_blob(P, cols, R, a0, a1, i);
 }
 
 // Fixed-layout decode (the transpose of k_encode_fixed_dw).  A workgroup
@@ -1373,7 +1445,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecPro
     if (!__syncthreads_and(ok)) {
         for (uint32_t j = tid; j < rows; j += kBlock) {
             const uint64_t i = blob0 + j;
-            status[i] = decode_blob(P, cols, arena, offs[i], offs[i + 1], i);
+            status[i] = decode_blob(P, cols, GReader{arena}, offs[i], offs[i + 1], i);
         }
         return;
     }
@@ -1455,7 +1527,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecPro
     for (uint32_t j = tid; j < rows; j += kBlock) {
         const uint64_t i = blob0 + j;
         uint32_t sv = 0;
-        if (fail[j]) sv = decode_blob(P, cols, arena, offs ? offs[i] : i * B, offs ? offs[i + 1] : (i + 1) * B, i);
+        if (fail[j]) sv = decode_blob(P, cols, GReader{arena}, offs ? offs[i] : i * B, offs ? offs[i + 1] : (i + 1) * B, i);
         status[i] = sv;
     }
 }
@@ -1573,7 +1645,7 @@ bool packos::canonical_decodes(const packos_schema* s) {
         dc.length[c] = &length[c];
     }
     DecProgram P{s->dnodes.data(), s->dkids.data(), s->lits.data(), 0};
-    return decode_blob(P, dc, s->canon.data(), 0, s->canon.size(), 0) == 0;
+    return decode_blob(P, dc, GReader{s->canon.data()}, 0, s->canon.size(), 0) == 0;
 }
 
 namespace {
@@ -1966,8 +2038,11 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
         const size_t lds = (size_t)T * B + 16 + 8 * QW + 4 * ((T + 1) & ~1u) + 32 * s->dfix.size();
         hipLaunchKernelGGL(k_decode_fixed, dim3((unsigned)((n + T - 1) / T)), dim3(kBlock), lds, st, t->dfix, t->dec,
                            dc, arena, offsets, (uint64_t)n, status);
-    } else {
+    } else if (getenv("PACKOS_DECODE_NOWIN")) {
         hipLaunchKernelGGL(k_decode, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, t->dec, dc,
+                           arena, offsets, stride, (uint64_t)n, status);
+    } else {
+        hipLaunchKernelGGL(k_decode_win, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, t->dec, dc,
                            arena, offsets, stride, (uint64_t)n, status);
     }
     HIP_TRY(hipGetLastError());

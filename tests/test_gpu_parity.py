@@ -277,6 +277,25 @@ def test_random_decode_corrupted(seed):
     assert_same_decode(chain, arena2, np.asarray(noffs, np.uint64), n, f"corrupt seed {seed}")
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_decode_without_window(seed, monkeypatch):
+    """PACKOS_DECODE_NOWIN: the plain thread-per-blob decoder (no LDS window)
+    on clean and corrupted batches must agree with the oracle too."""
+    monkeypatch.setenv("PACKOS_DECODE_NOWIN", "1")
+    monkeypatch.setenv("PACKOS_DECODE_GENERIC", "1")
+    rng = np.random.default_rng(77 + seed)
+    chain = rand_chain(seed)
+    hc = HostColumns.from_rows(chain, rand_rows(chain, 300, seed + 3))
+    arena, offs, _ = ob.encode(chain, hc, 0)
+    assert_same_decode(chain, arena, offs, hc.n, f"nowin seed {seed}")
+    arena = arena.copy()
+    for i in range(0, hc.n, 4):
+        a, b = int(offs[i]), int(offs[i + 1])
+        if b > a:
+            arena[a + int(rng.integers(0, min(b - a, 16)))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    assert_same_decode(chain, arena, offs, hc.n, f"nowin corrupt seed {seed}")
+
+
 @pytest.mark.parametrize("seed", range(30))
 def test_fixed_decode_fast_path(seed):
     """Fixed-size schemas take the tiled fast path (k_decode_fixed).  In-place

@@ -1,8 +1,11 @@
-# Tile-size sweep of the tiled var encode (after the parity suite passed).
+# Tile-size / LDS-budget sweep of the tiled var encode (run after the parity suite).
+# SWEEP="vt,bud,in;vt,bud,in;..."
 set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-for vt in 64 128 256; do
-  PACKOS_VAR_TILE=$vt timeout -k 10 300 python tools/vbench.py ${VB_ARGS:-C3 C5} > gpurun_out/vsweep_$vt.log 2>&1 || exit $?
-  echo "VT=$vt"; grep -v amdgpu.ids gpurun_out/vsweep_$vt.log
+IFS=';' read -ra CFGS <<< "${SWEEP:-128,16384,16384;256,16384,16384;128,8192,12288;128,8192,8192}"
+for cfg in "${CFGS[@]}"; do
+  IFS=',' read -r vt bud inb <<< "$cfg"
+  PACKOS_VAR_TILE=$vt PACKOS_VAR_BUD=$bud PACKOS_VAR_IN=$inb timeout -k 10 300 python tools/vbench.py ${VB_ARGS:-C3 C5} > gpurun_out/vsweep.log 2>&1 || exit $?
+  echo "VT=$vt bud=$bud in=$inb"; grep -v amdgpu.ids gpurun_out/vsweep.log | sed 's/, "decode.*//'
 done
