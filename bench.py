@@ -100,12 +100,10 @@ def main():
     total_out = r.total
     out = r.arena
 
-    if fixed:
-        plan = EncodePlan(schema, dcols, out=out, stream=stream)
-        step = plan.run
-    else:
-        def step():
-            encode_batch(schema, dcols, want_offsets=True, want_status=False, out=out)
+    # one step = one plan replay: fixed -> one encode launch; var -> size pass +
+    # scan + encode, all on `stream`, no host sync
+    plan = EncodePlan(schema, dcols, out=out, stream=stream)
+    step = plan.run
 
     for _ in range(args.warmup):
         step()

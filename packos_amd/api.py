@@ -208,28 +208,59 @@ def encode_batch(schema: CompiledSchema, cols: DeviceColumns, want_offsets: bool
 
 
 class EncodePlan:
-    """Pre-bound encode of a fixed-size batch into a preallocated arena: one
-    C-ABI call per run() (what a serving loop or graph capture replays)."""
+    """Pre-bound encode of one batch into a preallocated arena: run() issues
+    only C-ABI calls on `stream` (no host sync, no allocation) — what a serving
+    loop or a graph capture replays.  Fixed-size batches: one encode call.
+    Variable-size batches: the size pass + scan, then the encode with
+    PACKOS_ENC_OFFSETS_READY; the arena is sized once at construction (one
+    host sync there) and `offsets` / `status` are refreshed by every run()."""
 
-    def __init__(self, schema: CompiledSchema, cols: DeviceColumns, out=None, stream=None, flags: int = 0):
+    def __init__(self, schema: CompiledSchema, cols: DeviceColumns, out=None, stream=None, flags: int = 0,
+                 want_status: bool = False):
         torch = _torch()
+        L = lib()
         self.flags = flags
-        if cols.has_var() or cols.any_valid():
-            raise ValueError("EncodePlan is for fixed-size batches")
         self.schema, self.cols = schema, cols
-        self.B = schema.all_present_size()
-        self.total = self.B * cols.n
-        dev = cols.data[0].device
-        self.out = out if out is not None else torch.empty(max(self.total, 16), dtype=torch.uint8, device=dev)
+        n = cols.n
+        dev = cols.data[0].device if cols.data and cols.data[0] is not None else torch.device("cuda")
+        self.fixed = (not cols.has_var()) and not cols.any_valid()
         self._arr = cols.ctypes_array()
         self._stream = stream
-        self._args = None
+        self.status = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if want_status else None
+        if self.fixed:
+            self.B = schema.all_present_size()
+            self.total = self.B * n
+            self.offsets = None
+            self.ws, self.wsb = None, 0
+        else:
+            self.B = -1
+            self.offsets = torch.empty(n + 1, dtype=torch.int64, device=dev)
+            self.wsb = L.packos_encode_workspace_size(schema.handle, n)
+            self.ws = torch.empty(max(self.wsb, 16), dtype=torch.uint8, device=dev)
+            check(L.packos_encoded_size_batch(schema.handle, self._arr, n, self.offsets.data_ptr(),
+                                              self.ws.data_ptr(), self.wsb, _stream_ptr(stream)),
+                  "packos_encoded_size_batch")
+            if stream is not None:
+                stream.synchronize()
+            self.total = int(self.offsets[n].item()) if n else 0
+        self.out = out if out is not None else torch.empty(max(self.total, 16), dtype=torch.uint8, device=dev)
+        if self.out.numel() < self.total:
+            raise ValueError("EncodePlan: `out` is smaller than the batch's encoded size")
 
     def run(self):
+        L = lib()
         st = _stream_ptr(self._stream)
-        check(lib().packos_encode_batch(self.schema.handle, self._arr, self.cols.n, self.out.data_ptr(),
-                                        self.out.numel(), None, None, None, 0, self.flags, st),
-              "packos_encode_batch")
+        n = self.cols.n
+        stp = None if self.status is None else self.status.data_ptr()
+        if self.fixed:
+            check(L.packos_encode_batch(self.schema.handle, self._arr, n, self.out.data_ptr(), self.out.numel(),
+                                        None, stp, None, 0, self.flags, st), "packos_encode_batch")
+            return self.out
+        check(L.packos_encoded_size_batch(self.schema.handle, self._arr, n, self.offsets.data_ptr(),
+                                          self.ws.data_ptr(), self.wsb, st), "packos_encoded_size_batch")
+        check(L.packos_encode_batch(self.schema.handle, self._arr, n, self.out.data_ptr(), self.out.numel(),
+                                    self.offsets.data_ptr(), stp, self.ws.data_ptr(), self.wsb,
+                                    _lib.ENC_OFFSETS_READY | self.flags, st), "packos_encode_batch")
         return self.out
 
 
