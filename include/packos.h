@@ -178,7 +178,12 @@ int64_t packos_schema_blob_size_host(const packos_schema* s, const uint32_t* wid
 
 /* ---- batch encode ---------------------------------------------------------- */
 
-/* Workspace (device memory) a batch of n blobs needs. */
+/* Device scratch a variable-size batch of n blobs needs: scan tile sums
+ * (size pass), per-tile flags and per-blob value positions of the tiled
+ * variable-size encoder.  packos_encoded_size_batch requires it;
+ * packos_encode_batch uses it when given (without it, a variable-size batch
+ * with PACKOS_ENC_OFFSETS_READY runs the slower one-wavefront-per-blob
+ * kernel).  Fixed-size batches need none. */
 size_t packos_encode_workspace_size(const packos_schema* s, size_t n_blobs);
 
 /* Size pass + exclusive scan: out_offsets[0..n] (device, uint64).  Fixed-size

@@ -313,10 +313,23 @@ struct Builder {
         if (s->items.size() > 65000) fail(PACKOS_E_UNSUPPORTED, "schema too large");
         // per-item kernel aux data: var slot, staging region, divide magic
         int nv = 0, nr = 0;
+        s->ipk.clear();
         for (EncItem& it : s->items) {
             it.vslot = it.type == IT_VAR ? (uint8_t)std::min(nv++, 255) : 0;
             it.reg = it.type == IT_FIXED ? (uint8_t)std::min(nr++, 255) : 255;
             it.magic = it.size > 1 ? (uint32_t)(((1ull << 32) + it.size - 1) / it.size) : 0u;
+            const uint32_t vs = it.type == IT_VAR ? it.vslot : 255u;
+            s->ipk.push_back((std::min<uint32_t>(it.size, 0xFFFFu)) | (vs << 16));
+        }
+        // header entries of each header item: contiguous, j ascending (emit_container)
+        s->ihr.assign(s->items.size(), 0u);
+        for (size_t h = 0; h < s->hdrs.size(); h++) {
+            const EncHdr& e = s->hdrs[h];
+            uint32_t& r = s->ihr[e.hdr_item];
+            if ((r >> 16) == 0) r = (uint32_t)h;
+            if ((r & 0xFFFFu) + (r >> 16) != h || e.j != (r >> 16) || h > 0xFFFF)
+                fail(PACKOS_E_UNSUPPORTED, "internal: header entries not contiguous");
+            r += 1u << 16;
         }
     }
 

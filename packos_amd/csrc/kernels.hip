@@ -598,7 +598,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_var(EncProgram P, EncCols col
 //            dwords so that every thread keeps several loads in flight.
 // Tiles outside the plan (offsets that disagree with the program, a blob
 // > 64 KiB, capacity overrun) and runs > bud bytes use var_blob_wave.
-constexpr int kVBatch = 8;
+constexpr int kVBatch = 4;
 constexpr int kVPFix = 32;     // plan limits (more -> one wavefront per blob)
 constexpr int kVPVar = 16;
 constexpr int kVPVal = 16;
@@ -622,7 +622,7 @@ struct VVar {                  // var region of the current tile (LDS)
 };
 
 struct VtLayout {
-    uint32_t boff, pmk, bst, misc, subs, items, hdrs, conts, lits, voff, vld, pos, vvar, fmis, skip, stg, total;
+    uint32_t boff, pmk, bst, misc, subs, items, ipk, ihr, hdrs, conts, lits, voff, vld, pos, vvar, fmis, freg, stg, total;
 };
 __host__ __device__ inline VtLayout vt_layout(int VT, const EncProgram& P, int nvar, int nval, uint32_t bud,
                                                uint32_t in_bud) {
@@ -636,6 +636,8 @@ __host__ __device__ inline VtLayout vt_layout(int VT, const EncProgram& P, int n
     L.misc = o;  o += 4 * 16;
     L.subs = o;  o += al16(4 * (VT + 1));
     L.items = o; o += al16(sizeof(EncItem) * NI);
+    L.ipk = o;   o += al16(4 * NI);
+    L.ihr = o;   o += al16(4 * NI);
     L.hdrs = o;  o += al16(sizeof(EncHdr) * (uint32_t)P.n_hdrs);
     L.conts = o; o += al16(sizeof(EncCont) * (uint32_t)P.n_conts);
     L.lits = o;  o += al16((uint32_t)P.n_lits + 4);
@@ -644,11 +646,12 @@ __host__ __device__ inline VtLayout vt_layout(int VT, const EncProgram& P, int n
     L.pos = o;   o += al16(2 * VT * (NI + 1));
     L.vvar = o;  o += al16(sizeof(VVar) * nvar);
     L.fmis = o;  o += al16(4 * kVPFix);
-    L.skip = o;  o += al16(4 * ((bud + 32) / 16 / 32 + 1));
+    L.freg = o;  o += 16 * kVPFix;
     L.stg = o;   o += al16(in_bud + 16);
     L.total = o;
     return L;
 }
+
 
 __device__ __forceinline__ uint32_t magic_of(uint32_t d) {
     return d > 1 ? (uint32_t)((0x100000000ull + d - 1) / d) : 0u;
@@ -681,13 +684,14 @@ __global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCol
     EncItem* items = (EncItem*)(lds + L.items);
     EncHdr* hdrs = (EncHdr*)(lds + L.hdrs);
     EncCont* conts = (EncCont*)(lds + L.conts);
-    uint8_t* lits = lds + L.lits;
     uint32_t* voff = (uint32_t*)(lds + L.voff);
     uint8_t* vld = lds + L.vld;
     uint16_t* pos = (uint16_t*)(lds + L.pos);
     VVar* vvar = (VVar*)(lds + L.vvar);
     uint32_t* fmis = (uint32_t*)(lds + L.fmis);
-    uint32_t* skip = (uint32_t*)(lds + L.skip);   // run chunks k_var_copy writes
+    u32x4* freg = (u32x4*)(lds + L.freg);        // fixed region: {a0 lo, a0 hi, first chunk, LDS offset}
+    const uint32_t* ipk = (const uint32_t*)(lds + L.ipk);
+    const uint32_t* ihr = (const uint32_t*)(lds + L.ihr);
     uint8_t* stg = lds + L.stg;
 
     const uint64_t lo = (uint64_t)blockIdx.x * VT;
@@ -710,18 +714,31 @@ __global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCol
         const uint32_t e_items = (uint32_t)NI * (sizeof(EncItem) / 4);
         const uint32_t e_hdrs = e_items + (uint32_t)NH * (sizeof(EncHdr) / 4);
         const uint32_t e_conts = e_hdrs + (uint32_t)P.n_conts * (sizeof(EncCont) / 4);
-        const uint32_t e_lits = e_conts + ((uint32_t)P.n_lits + 3) / 4;
+        const uint32_t e_ipk = e_conts + (uint32_t)NI;
+        const uint32_t e_ihr = e_ipk + (uint32_t)NI;
+        const uint32_t e_lits = e_ihr + ((uint32_t)P.n_lits + 3) / 4;
         const uint32_t e_boff = e_lits + rows + 1;
         const uint32_t s_voff = al64(e_boff), S1 = al64(rows + 1);
         const uint32_t e_voff = s_voff + (uint32_t)V.nvar * S1;
         const uint32_t S0 = al64(rows);
         const uint32_t e_vld = e_voff + (uint32_t)V.nval * S0;
-        uint32_t fix_ch = 0;
-        for (int r = 0; r < V.nfix; r++) {
-            const uint64_t src = (uint64_t)(uintptr_t)(V.fix_ptr[r] + lo * V.fix_w[r]);
-            if (tid == 0) fmis[r] = V.fix_lds[r] + (uint32_t)(src & 15);
-            fix_ch += (uint32_t)(((src & 15) + (uint64_t)rows * V.fix_w[r] + 15) >> 4);
+        // fixed-region table, once per workgroup (lane r of wave 0; prefix by scan)
+        if (wave == 0) {
+            uint32_t nch = 0;
+            uint64_t src = 0;
+            if (lane < V.nfix) {
+                src = (uint64_t)(uintptr_t)V.fix_ptr[lane] + lo * V.fix_w[lane];
+                nch = (uint32_t)(((src & 15) + (uint64_t)rows * V.fix_w[lane] + 15) >> 4);
+            }
+            const uint32_t incl = wave_incl_scan(nch, lane);
+            if (lane < V.nfix) {
+                freg[lane] = u32x4{(uint32_t)(src & ~15ull), (uint32_t)(src >> 32), incl - nch, V.fix_lds[lane]};
+                fmis[lane] = V.fix_lds[lane] + (uint32_t)(src & 15);
+            }
+            if (lane == 63) misc[15] = incl;
         }
+        __syncthreads();
+        const uint32_t fix_ch = misc[15];
         const uint32_t E = e_vld + fix_ch;
         for (uint32_t e0 = tid; e0 < E; e0 += kVBatch * kBlock) {
             u32x4 v[kVBatch];
@@ -739,7 +756,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCol
                     if (e < e_items) { src = (const uint32_t*)P.items; x = e; dst[m] = L.items + 4 * x; }
                     else if (e < e_hdrs) { src = (const uint32_t*)P.hdrs; x = e - e_items; dst[m] = L.hdrs + 4 * x; }
                     else if (e < e_conts) { src = (const uint32_t*)P.conts; x = e - e_hdrs; dst[m] = L.conts + 4 * x; }
-                    else { src = (const uint32_t*)P.lits; x = e - e_conts; dst[m] = L.lits + 4 * x; }
+                    else if (e < e_ipk) { src = P.ipk; x = e - e_conts; dst[m] = L.ipk + 4 * x; }
+                    else if (e < e_ihr) { src = P.ihr; x = e - e_ipk; dst[m] = L.ihr + 4 * x; }
+                    else { src = (const uint32_t*)P.lits; x = e - e_ihr; dst[m] = L.lits + 4 * x; }
                     v[m].x = ((g_u32*)src)[x];
                     kind[m] = 1;
                 } else if (e < e_boff) {
@@ -767,19 +786,14 @@ __global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCol
                     kind[m] = 3;
                 } else {
                     const uint32_t c = e - e_vld;
-                    uint64_t a0 = 0;
-                    uint32_t cb = 0, base = 0, sel_lds = 0;
-                    for (int r = 0; r < V.nfix; r++) {
-                        const uint64_t src = (uint64_t)(uintptr_t)(V.fix_ptr[r] + lo * V.fix_w[r]);
-                        const uint32_t nch = (uint32_t)(((src & 15) + (uint64_t)rows * V.fix_w[r] + 15) >> 4);
-                        const bool in = c >= base;
-                        a0 = in ? (src & ~15ull) : a0;
-                        cb = in ? base : cb;
-                        sel_lds = in ? V.fix_lds[r] : sel_lds;
-                        base += nch;
+                    u32x4 g = freg[0];
+                    for (int r = 1; r < V.nfix; r++) {
+                        const u32x4 h = freg[r];
+                        if (c >= h.z) g = h;
                     }
-                    v[m] = *(const g_u32x4*)(uintptr_t)(a0 + 16ull * (c - cb));
-                    dst[m] = L.stg + sel_lds + 16 * (c - cb);
+                    const uint64_t a0 = ((uint64_t)g.y << 32) | g.x;
+                    v[m] = *(const g_u32x4*)(uintptr_t)(a0 + 16ull * (c - g.z));
+                    dst[m] = L.stg + g.w + 16 * (c - g.z);
                     kind[m] = 4;
                 }
             }
@@ -794,7 +808,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCol
                 }
             }
         }
-        if (tid < 16) misc[tid] = 0;
+        if (tid < 8) misc[tid] = 0;  // misc[15] (fixed chunk count) stays
     }
     __syncthreads();
     mark(0);
@@ -844,6 +858,30 @@ __global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCol
     };
     var_load(tid);
     // presence masks and item positions (LDS only)
+    if (V.nval == 0) {
+        // no validity columns: every container and leaf is present, so an
+        // item's size is static or its var value's length
+        const uint64_t pm_all = P.n_conts >= 64 ? ~0ull : ((1ull << P.n_conts) - 1ull);
+        for (uint32_t j = tid; j < rows; j += kBlock) {
+            pmk[j] = pm_all;
+            bst[j] = 0;
+            uint32_t p = 0;
+            uint16_t* pj = pos + j * NP;
+            for (int k = 0; k < NI; k++) {
+                const uint32_t x = ipk[k], vs = (x >> 16) & 0xFFu;
+                uint32_t sz = x & 0xFFFFu;
+                if (vs != 0xFFu) {
+                    const uint32_t* vo = voff + vs * (VT + 1);
+                    sz = vo[j + 1] - vo[j];
+                    if (sz > 0xFFFFu) sz = 0x10000u;
+                }
+                pj[k] = (uint16_t)p;
+                p += sz;
+            }
+            pj[NI] = (uint16_t)p;
+            if (p > 0xFFFFu || boff[j + 1] - boff[j] != p || boff[j] + p > cap) atomicOr(&misc[0], 1u);
+        }
+    } else
     for (uint32_t j = tid; j < rows; j += kBlock) {
         uint64_t pm = 0;
         for (int c = 0; c < P.n_conts; c++) {
@@ -896,7 +934,92 @@ __global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCol
             var_blob_wave(P, cols, lo + j, boff[j], out, cap, status, nullptr, wpos, lane);
         return;
     }
-    // ---- runs -----------------------------------------------------------------
+    uint32_t* L32 = (uint32_t*)lds;
+    if (any_direct) {
+        // ---- direct mode (long unstaged values, e.g. C5): no run buffer.  One
+        // thread per blob streams the blob's non-value bytes (header words,
+        // fixed and literal items, staged values) to HBM: whole dwords with
+        // dword stores, dwords shared with a neighbour or a value hole byte by
+        // byte.  k_var_copy then fills the holes.
+        for (uint32_t j = tid; j < rows; j += kBlock) {
+            const uint16_t* pj = pos + j * NP;
+            const uint64_t g0 = boff[j];
+            uint64_t acc = 0, D = g0 >> 2;
+            uint32_t ph = (uint32_t)(g0 & 3), sb = ph, ovf = 0;
+            auto flush_part = [&](uint32_t hi) {
+                for (uint32_t y = sb; y < hi; y++) out[4 * D + y] = (uint8_t)(acc >> (8 * y));
+            };
+            auto put = [&](uint32_t v, uint32_t nb) {
+                acc |= (uint64_t)v << (8 * ph);
+                ph += nb;
+                if (ph >= 4) {
+                    if (sb == 0) *(uint32_t*)(out + 4 * D) = (uint32_t)acc;
+                    else flush_part(4);
+                    sb = 0;
+                    D++;
+                    acc >>= 32;
+                    ph -= 4;
+                }
+            };
+            for (int k = 0; k < NI; k++) {
+                const uint32_t p0 = pj[k], len = (uint32_t)(pj[k + 1] - p0);
+                if (len == 0) continue;
+                const EncItem it = items[k];
+                if (it.type == IT_HDR) {
+                    const uint32_t hr = ihr[k], hb = hr & 0xFFFFu, cnt = hr >> 16;
+                    for (uint32_t e = 0; e < cnt; e++) {
+                        const EncHdr h = hdrs[hb + e];
+                        uint16_t v;
+                        if (h.relative) {
+                            const int64_t off = (int64_t)pj[h.target] - (int64_t)(p0 + len);
+                            ovf |= off >= 8192;
+                            v = enc_header(off, h.tag);
+                        } else {
+                            v = h.value;
+                            ovf |= h.ovf != 0;
+                        }
+                        put(v, 2);
+                    }
+                    continue;
+                }
+                uint32_t so;
+                if (it.type == IT_CONST) {
+                    so = L.lits + it.lit;
+                } else if (it.type == IT_FIXED) {
+                    so = L.stg + fmis[it.reg] + j * it.size;
+                } else {
+                    const VVar g = vvar[it.vslot];
+                    const uint32_t* vo = voff + it.vslot * (VT + 1);
+                    if (g.lds_off == UINT32_MAX) {  // hole for k_var_copy
+                        if (ph > sb) flush_part(ph);
+                        const uint64_t dn = 4 * D + ph + len;
+                        D = dn >> 2;
+                        ph = sb = (uint32_t)(dn & 3);
+                        acc = 0;
+                        continue;
+                    }
+                    so = L.stg + g.lds_off + (uint32_t)(g.src & 15) + (vo[j] - vo[0]);
+                }
+                if (it.is_bool) {
+                    put(lds[so] != 0 ? 1u : 0u, 1);
+                    continue;
+                }
+                for (uint32_t x = 0; x < len; x += 4) {
+                    const uint32_t nb = min(4u, len - x);
+                    const uint32_t sa = so + x, wi = sa >> 2;
+                    uint32_t v = __builtin_amdgcn_alignbyte(L32[wi + 1], L32[wi], sa & 3);
+                    if (nb < 4) v &= (1u << (8 * nb)) - 1u;
+                    put(v, nb);
+                }
+            }
+            const uint32_t tot = (uint32_t)(boff[j + 1] - boff[j]);
+            for (uint32_t x = pj[NI]; x < tot; x += 4) put(0u, min(4u, tot - x));
+            if (ph > sb) flush_part(ph);
+            if (ovf) bst[j] |= 1u;
+        }
+        mark(2);
+    } else {
+    // ---- runs (everything staged, e.g. C3) --------------------------------------
     {
         const uint32_t j = tid;
         const uint32_t win = j < rows ? (uint32_t)((boff[j] - boff[0]) >> win_shift) : 0u;
@@ -934,11 +1057,10 @@ __global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCol
         }
         const uint32_t nch = (nb + 15) >> 4;
         for (uint32_t c = tid; c < nch; c += kBlock) ((u32x4*)obuf)[c] = u32x4{0u, 0u, 0u, 0u};
-        if (any_direct)
-            for (uint32_t c = tid; c < (nch + 31) / 32; c += kBlock) skip[c] = 0u;
         __syncthreads();
+        mark(5);
         const uint32_t nbr = b - a, nb_mag = magic_of(nbr);
-        // header words: (header, blob) pairs
+        // header words: (header, blob) pairs, OR-ed into the zeroed buffer
         for (uint32_t t = tid; t < nbr * (uint32_t)NH; t += kBlock) {
             const uint32_t hh = fast_div(t, nbr, nb_mag), j = a + (t - hh * nbr);
             const EncHdr h = hdrs[hh];
@@ -957,10 +1079,16 @@ __global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCol
             }
             if (ovf) atomicOr(&bst[j], 1u);
             const uint32_t d = (uint32_t)(boff[j] - al) + hpos + 2 * h.j;
-            obuf[d] = (uint8_t)v;
-            obuf[d + 1] = (uint8_t)(v >> 8);
+            const uint32_t sh = 8 * (d & 3);
+            if (sh <= 16) {
+                atomicOr(L32 + (d >> 2), (uint32_t)v << sh);
+            } else {
+                atomicOr(L32 + (d >> 2), ((uint32_t)v & 0xFFu) << 24);
+                atomicOr(L32 + (d >> 2) + 1, (uint32_t)v >> 8);
+            }
         }
-        // items: (item, blob) pairs, item-major
+        // items: (item, blob) pairs, item-major; whole destination dwords
+        // stored, partial ones OR-ed; sources funnel-shifted from LDS
         for (uint32_t t = tid; t < nbr * (uint32_t)NI; t += kBlock) {
             const uint32_t k = fast_div(t, nbr, nb_mag), j = a + (t - k * nbr);
             const EncItem it = items[k];
@@ -968,38 +1096,39 @@ __global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCol
             const uint16_t* pj = pos + j * NP;
             const uint32_t p0 = pj[k], len = (uint32_t)(pj[k + 1] - p0);
             if (len == 0) continue;
-            uint8_t* d = obuf + (uint32_t)(boff[j] - al) + p0;
-            const uint8_t* sp;
+            const uint32_t d = (uint32_t)(boff[j] - al) + p0;
+            uint32_t so;
             if (it.type == IT_CONST) {
-                sp = lits + it.lit;
+                so = L.lits + it.lit;
             } else if (it.type == IT_FIXED) {
-                sp = stg + fmis[it.reg] + j * it.size;
+                so = L.stg + fmis[it.reg] + j * it.size;
             } else {
                 const VVar g = vvar[it.vslot];
-                if (g.lds_off == UINT32_MAX) {  // k_var_copy writes the value: mark its whole chunks
-                    const uint32_t rel = (uint32_t)(boff[j] - al) + p0;
-                    const uint32_t c0 = (rel + 15) >> 4, c1 = (rel + len) >> 4;
-                    for (uint32_t w = c0 >> 5; c0 < c1 && w <= (c1 - 1) >> 5; w++) {
-                        const uint32_t b0 = max(c0, w * 32) - w * 32, b1 = min(c1, w * 32 + 32) - w * 32;
-                        const uint32_t mask = (b1 - b0 == 32) ? ~0u : (((1u << (b1 - b0)) - 1u) << b0);
-                        atomicOr(&skip[w], mask);
-                    }
-                    continue;
-                }
-                sp = stg + g.lds_off + (uint32_t)(g.src & 15) + (voff[it.vslot * (VT + 1) + j] - voff[it.vslot * (VT + 1)]);
+                so = L.stg + g.lds_off + (uint32_t)(g.src & 15) + (voff[it.vslot * (VT + 1) + j] - voff[it.vslot * (VT + 1)]);
             }
             if (it.is_bool) {
-                d[0] = sp[0] != 0;
-            } else {
-#pragma unroll 4
-                for (uint32_t x = 0; x < len; x++) d[x] = sp[x];
+                atomicOr(L32 + (d >> 2), (uint32_t)(lds[so] != 0) << (8 * (d & 3)));
+                continue;
+            }
+            const uint32_t D0 = d >> 2, D1 = (d + len - 1) >> 2;
+            for (uint32_t D = D0; D <= D1; D++) {
+                const uint32_t sa = so + 4 * D - d;
+                const uint32_t wi = sa >> 2;
+                const uint32_t v = __builtin_amdgcn_alignbyte(L32[wi + 1], L32[wi], sa & 3);
+                const uint32_t b0 = 4 * D < d ? d - 4 * D : 0u, b1 = min(4u, d + len - 4 * D);
+                if (b0 == 0 && b1 == 4) {
+                    L32[D] = v;
+                } else {
+                    const uint32_t m = (b1 == 4 ? ~0u : ((1u << (8 * b1)) - 1u)) & ~((1u << (8 * b0)) - 1u);
+                    atomicOr(L32 + D, v & m);
+                }
             }
         }
         __syncthreads();
+        mark(6);
         // write [s0, s1)
         for (uint32_t c = tid; c < nch; c += kBlock) {
             const uint64_t g0 = al + 16ull * c;
-            if (any_direct && ((skip[c >> 5] >> (c & 31)) & 1u)) continue;
             if (g0 >= s0 && g0 + 16 <= s1) {
                 __builtin_nontemporal_store(((const u32x4*)obuf)[c], (u32x4*)(out + g0));
             } else {
@@ -1010,6 +1139,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCol
             }
         }
         __syncthreads();
+        mark(7);
+    }
     }
     mark(3);
     // ---- unstaged var values: hand their positions to k_var_copy -------------
@@ -1686,6 +1817,8 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
         if (d.device == device) { *out = &d; return PACKOS_OK; }
     std::vector<uint8_t> blob;
     size_t o_items = put_bytes(blob, s->items);
+    size_t o_ipk = put_bytes(blob, s->ipk);
+    size_t o_ihr = put_bytes(blob, s->ihr);
     size_t o_hdrs = put_bytes(blob, s->hdrs);
     size_t o_conts = put_bytes(blob, s->conts);
     size_t o_lits = put_bytes(blob, s->lits);
@@ -1703,6 +1836,8 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     HIP_TRY(hipMemcpy(t.block, blob.data(), blob.size(), hipMemcpyHostToDevice));
     uint8_t* b = (uint8_t*)t.block;
     t.enc.items = (const EncItem*)(b + o_items);
+    t.enc.ipk = (const uint32_t*)(b + o_ipk);
+    t.enc.ihr = (const uint32_t*)(b + o_ihr);
     t.enc.hdrs = (const EncHdr*)(b + o_hdrs);
     t.enc.conts = (const EncCont*)(b + o_conts);
     t.enc.lits = b + o_lits;
@@ -1985,7 +2120,7 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
             HIP_TRY(hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
             fprintf(stderr, "var_tile vt=%d lds=%zu blocks=%u ticks/block:", vt, l, g.x);
-            for (int i = 0; i < 5; i++) fprintf(stderr, " p%d=%.0f", i, (double)h[i] / g.x);
+            for (int i = 0; i < 8; i++) fprintf(stderr, " p%d=%.0f", i, (double)h[i] / g.x);
             fprintf(stderr, "\n");
         }
         return PACKOS_OK;

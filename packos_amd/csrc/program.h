@@ -61,6 +61,8 @@ struct EncProgram {
     const uint8_t* lits;
     int32_t n_items, n_hdrs, n_conts, mode;
     int32_t n_lits;
+    const uint32_t* ipk;   // per item: bits 0-15 static size, 16-23 var slot (255 = not var)
+    const uint32_t* ihr;   // per item: IT_HDR -> first header entry | count << 16
 };
 
 // Fixed-size layout (no var-width leaves, no nils in the call): every blob is

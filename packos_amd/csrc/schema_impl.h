@@ -44,6 +44,8 @@ struct packos_schema {
 
     // encode program (host copies)
     std::vector<packos::EncItem> items;
+    std::vector<uint32_t> ipk;           // packed per-item size / var slot (EncProgram::ipk)
+    std::vector<uint32_t> ihr;           // per-item header-entry range (EncProgram::ihr)
     std::vector<packos::EncHdr> hdrs;
     std::vector<packos::EncCont> conts;
     std::vector<uint8_t> lits;
