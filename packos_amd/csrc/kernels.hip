@@ -1170,6 +1170,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCol
 // chunks of a value go byte by byte.  Runs after k_encode_var_tile, which
 // skipped the whole chunks and wrote the edge chunks' other bytes.
 constexpr int kCopyBatch = 4;
+// (Measured on MI355X, C5: loading a whole chunk's source with one dwordx4
+// at a byte-misaligned address is 1.5x slower, at a dword-aligned address
+// 1.3x slower, than two 16-B-aligned loads + the funnel below.)
 
 __device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     return q == 0 ? a : q == 1 ? b : q == 2 ? c : d;
@@ -1218,33 +1221,40 @@ __global__ __launch_bounds__(kBlock) void k_var_copy(VarPlan V, const uint64_t* 
         }
         const uint32_t U = uo[rows];
         const uint8_t* col = V.var_data[v];
-        for (uint32_t u0 = tid; u0 < U; u0 += kCopyBatch * kBlock) {
+        // each wavefront takes 64 * kCopyBatch consecutive units per step; one
+        // (wave-uniform) binary search for the step's first unit, then each
+        // lane walks forward to its units' blobs
+        for (uint32_t ub = wave * (kWave * kCopyBatch); ub < U; ub += kWavesPerBlock * kWave * kCopyBatch) {
+            uint32_t jw;
+            {
+                uint32_t l = 0, r = rows - 1;  // last blob j with uo[j] <= ub
+                while (l < r) {
+                    const uint32_t mm = (l + r + 1) >> 1;
+                    if (uo[mm] <= ub) l = mm; else r = mm - 1;
+                }
+                jw = l;
+            }
             u32x4 a[kCopyBatch], b[kCopyBatch];
             uint64_t dst[kCopyBatch];
             uint32_t sh[kCopyBatch], k0[kCopyBatch], k1[kCopyBatch];
+            uint32_t j = jw;
 #pragma unroll
             for (int m = 0; m < kCopyBatch; m++) {
-                const uint32_t u = u0 + m * kBlock;
+                const uint32_t u = ub + lane + kWave * m;
                 k0[m] = k1[m] = 0;
                 sh[m] = 0;
                 dst[m] = 0;
                 a[m] = b[m] = u32x4{0u, 0u, 0u, 0u};
                 if (u >= U) continue;
-                uint32_t l = 0, r = rows - 1;  // last blob j with uo[j] <= u
-                while (l < r) {
-                    const uint32_t mm = (l + r + 1) >> 1;
-                    if (uo[mm] <= u) l = mm; else r = mm - 1;
-                }
-                const uint64_t d0 = boff[l] + ps[l];
-                const uint32_t ln = vo[l + 1] - vo[l];
-                const uint64_t C = 16 * ((d0 >> 4) + (u - uo[l]));
+                while (uo[j + 1] <= u) j++;
+                const uint64_t d0 = boff[j] + ps[j];
+                const uint32_t ln = vo[j + 1] - vo[j];
+                const uint64_t C = 16 * ((d0 >> 4) + (u - uo[j]));
                 dst[m] = C;
-                // chunk bytes [k0, k1) belong to the value
                 k0[m] = C >= d0 ? 0u : (uint32_t)(d0 - C);
                 k1[m] = (uint32_t)min((uint64_t)16, d0 + ln - C);
-                // source of chunk byte 0 (may lie outside the value for an edge chunk:
-                // only the aligned blocks that hold needed bytes are read)
-                const uintptr_t xa = (uintptr_t)(col + vo[l]) + (uintptr_t)(C - d0);
+                const uintptr_t xa = (uintptr_t)(col + vo[j]) + (uintptr_t)(C - d0);
+                // aligned blocks holding needed bytes only (edge chunks may need one)
                 const g_u32x4* xw = (const g_u32x4*)(xa & ~(uintptr_t)15);
                 sh[m] = (uint32_t)(xa & 15);
                 if (k0[m] < 16 - sh[m]) a[m] = xw[0];
@@ -1252,7 +1262,7 @@ __global__ __launch_bounds__(kBlock) void k_var_copy(VarPlan V, const uint64_t* 
             }
 #pragma unroll
             for (int m = 0; m < kCopyBatch; m++) {
-                if (u0 + m * kBlock >= U) continue;
+                if (k1[m] <= k0[m]) continue;
                 u32x4 o4;
                 if (sh[m] == 0) {
                     o4 = a[m];
@@ -1262,18 +1272,25 @@ __global__ __launch_bounds__(kBlock) void k_var_copy(VarPlan V, const uint64_t* 
                     uint32_t t5[5];
 #pragma unroll
                     for (int i = 0; i < 5; i++) t5[i] = sel4(q, w[i], w[i + 1], w[i + 2], w[i + 3]);
-                    o4.x = sb ? __builtin_amdgcn_alignbyte(t5[1], t5[0], sb) : t5[0];
-                    o4.y = sb ? __builtin_amdgcn_alignbyte(t5[2], t5[1], sb) : t5[1];
-                    o4.z = sb ? __builtin_amdgcn_alignbyte(t5[3], t5[2], sb) : t5[2];
-                    o4.w = sb ? __builtin_amdgcn_alignbyte(t5[4], t5[3], sb) : t5[3];
+                    o4.x = __builtin_amdgcn_alignbyte(t5[1], t5[0], sb);
+                    o4.y = __builtin_amdgcn_alignbyte(t5[2], t5[1], sb);
+                    o4.z = __builtin_amdgcn_alignbyte(t5[3], t5[2], sb);
+                    o4.w = __builtin_amdgcn_alignbyte(t5[4], t5[3], sb);
                 }
                 if (k0[m] == 0 && k1[m] == 16) {
                     __builtin_nontemporal_store(o4, (u32x4*)(out + dst[m]));
                 } else {
                     const uint32_t wv[4] = {o4.x, o4.y, o4.z, o4.w};
 #pragma unroll
-                    for (int x = 0; x < 16; x++)
-                        if ((uint32_t)x >= k0[m] && (uint32_t)x < k1[m]) out[dst[m] + x] = (uint8_t)(wv[x >> 2] >> (8 * (x & 3)));
+                    for (int i = 0; i < 4; i++) {
+                        const uint32_t lo4 = 4 * i, s4 = max(k0[m], lo4), e4 = min(k1[m], lo4 + 4);
+                        if (s4 >= e4) continue;
+                        if (s4 == lo4 && e4 == lo4 + 4) {
+                            *(uint32_t*)(out + dst[m] + lo4) = wv[i];
+                        } else {
+                            for (uint32_t y = s4; y < e4; y++) out[dst[m] + y] = (uint8_t)(wv[i] >> (8 * (y - lo4)));
+                        }
+                    }
                 }
             }
         }
