@@ -1522,7 +1522,15 @@ __global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols col
                                                        const uint64_t* __restrict__ offs, uint64_t stride, uint64_t n,
                                                        uint32_t* __restrict__ status) {
     __shared__ __attribute__((aligned(16))) uint8_t win[kBlock * kDecWinChunks * 16];
+    extern __shared__ __attribute__((aligned(16))) uint8_t ptab[];   // decode program copy (nodes | kids | lits)
     const int tid = threadIdx.x;
+    // the program is read once per visited field: keep it in LDS
+    DecNode* lnodes = (DecNode*)ptab;
+    int32_t* lkids = (int32_t*)(ptab + ((P.n_nodes * sizeof(DecNode) + 15) & ~15));
+    uint8_t* llits = (uint8_t*)lkids + ((P.n_kids * 4 + 15) & ~15);
+    for (int x = tid; x < P.n_nodes; x += kBlock) lnodes[x] = P.nodes[x];
+    for (int x = tid; x < P.n_kids; x += kBlock) lkids[x] = P.kids[x];
+    for (int x = tid; x < P.n_lits; x += kBlock) llits[x] = P.lits[x];
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + tid;
     uint64_t a0 = 0, a1 = 0;
     if (i < n) {
@@ -1540,9 +1548,11 @@ __global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols col
 #pragma unroll
     for (int c = 0; c < kDecWinChunks; c++)
         if ((uint32_t)c < nch) *(u32x4*)(w + 16 * c) = v[c];
+    __syncthreads();
     if (i >= n) return;
     const WReader R{arena, w, b0, 16 * nch};
-    status[i] = decode_blob(P, cols, R, a0, a1, i);
+    const DecProgram LP{lnodes, lkids, llits, P.root, P.n_nodes, P.n_kids, P.n_lits};
+    status[i] = decode_blob(LP, cols, R, a0, a1, i);
 }
 
 // Fixed-layout decode (the transpose of k_encode_fixed_dw).  A workgroup
@@ -1792,7 +1802,8 @@ bool packos::canonical_decodes(const packos_schema* s) {
         dc.start[c] = &start[c];
         dc.length[c] = &length[c];
     }
-    DecProgram P{s->dnodes.data(), s->dkids.data(), s->lits.data(), 0};
+    DecProgram P{s->dnodes.data(), s->dkids.data(), s->lits.data(), 0, (int32_t)s->dnodes.size(),
+                 (int32_t)s->dkids.size(), (int32_t)s->lits.size()};
     return decode_blob(P, dc, GReader{s->canon.data()}, 0, s->canon.size(), 0) == 0;
 }
 
@@ -1877,6 +1888,9 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     t.dec.kids = (const int32_t*)(b + o_dkids);
     t.dec.lits = b + o_lits;
     t.dec.root = 0;
+    t.dec.n_nodes = (int32_t)s->dnodes.size();
+    t.dec.n_kids = (int32_t)s->dkids.size();
+    t.dec.n_lits = (int32_t)s->lits.size();
     t.dfix.cols = (const DecFix*)(b + o_dfix);
     t.dfix.chk = (const uint32_t*)(b + o_dchk);
     t.dfix.B = (int)s->all_present_size;
@@ -2194,8 +2208,10 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
         hipLaunchKernelGGL(k_decode, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, t->dec, dc,
                            arena, offsets, stride, (uint64_t)n, status);
     } else {
-        hipLaunchKernelGGL(k_decode_win, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, t->dec, dc,
-                           arena, offsets, stride, (uint64_t)n, status);
+        const size_t ptab = ((s->dnodes.size() * sizeof(DecNode) + 15) & ~(size_t)15) +
+                            ((s->dkids.size() * 4 + 15) & ~(size_t)15) + s->lits.size() + 16;
+        hipLaunchKernelGGL(k_decode_win, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), ptab, st, t->dec,
+                           dc, arena, offsets, stride, (uint64_t)n, status);
     }
     HIP_TRY(hipGetLastError());
     return PACKOS_OK;

@@ -128,6 +128,7 @@ struct DecProgram {
     const int32_t* kids;
     const uint8_t* lits;
     int32_t root;
+    int32_t n_nodes, n_kids, n_lits;   // table sizes (for staging into LDS)
 };
 
 // Fixed-layout decode fast path.  A blob whose length is B and whose
