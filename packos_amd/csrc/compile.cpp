@@ -396,6 +396,7 @@ struct Builder {
             fc.width = (uint32_t)n.width;
             fc.lds_off = lds;
             fc.chunk_begin = chunks;
+            fc.flags = n.kind == K_BOOL ? 1u : 0u;
             lds_of_col[c] = (int)lds;
             uint32_t bytes = (uint32_t)T * fc.width;
             chunks += bytes / 16;
@@ -486,6 +487,7 @@ struct Builder {
         // lane-invariant per-dword descriptors (blob-relative; B % 4 == 0 means
         // no dword straddles two blobs)
         s->fdw.clear();
+        s->fix_maxseg = 0;
         if (B % 4 == 0) {
             for (int64_t q = 0; q < B / 4; q++) {
                 DwDesc dd{};
@@ -512,6 +514,7 @@ struct Builder {
                     b = b1;
                 }
                 s->fdw.push_back(dd);
+                s->fix_maxseg = std::max<int>(s->fix_maxseg, (int)dd.nseg);
             }
         }
         // tile + descriptor tables must fit the 64 KiB dynamic LDS of one launch

@@ -211,6 +211,166 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCol
     }
 }
 
+// Pipelined lane-invariant form (default for fixed schemas with B % 4 == 0).
+// A grid of ~CUs x 8 workgroups walks the full tiles (tile = blockIdx.x,
+// + gridDim.x, ...).  Per tile: the input registers fetched during the
+// previous tile's assembly go to LDS (bool columns normalised to 0/1 here, so
+// assembly needs no per-segment flag test), the NEXT tile's loads are issued,
+// then each thread builds its output dwords from LDS (<= MAXSEG sources, all
+// padded to MAXSEG so the inner loop is branch-free) and stores them NT.  So
+// every workgroup keeps a tile of loads in flight while it assembles and
+// stores, and the staging plan (which column chunk each of a thread's 4 slots
+// fetches; from kernarg, no dependent table read before the first loads) and
+// the dword descriptors are set up once per workgroup, not once per tile.
+// The partial last tile (n % T blobs) goes through stage_tile + the flagged
+// dword loop of k_encode_fixed_dw in the workgroup that would own it.
+// Measured against k_encode_fixed_dw: PMC showed ~790 VALU per wave per tile
+// there (column walk + 4-way flagged segment loop), the bulk of the kernel.
+template <int MAXSEG, int PER>
+__global__ __launch_bounds__(kBlock) void k_encode_fixed_pipe(FixProgram P, FixStage S, EncCols cols,
+                                                              uint8_t* __restrict__ out, uint64_t n,
+                                                              uint32_t* __restrict__ status, uint32_t st_val) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t T = (uint32_t)P.T;
+    const uint32_t B = (uint32_t)P.B;
+    const uint32_t Q4 = B >> 2;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t q = tid % Q4, s = tid / Q4, R = kBlock / Q4;
+    const uint64_t nfull = n / T;
+
+    // ---- staging plan: slot u of this thread = chunk u*256 + tid of a tile
+    const uint8_t* src[kStageSlots];
+    uint32_t step[kStageSlots], dst[kStageSlots];
+    uint32_t okm = 0, boolm = 0;
+#pragma unroll
+    for (int u = 0; u < kStageSlots; u++) {
+        const uint32_t k = (uint32_t)u * kBlock + tid;
+        const uint8_t* base = nullptr;
+        uint32_t w = 0, lo = 0, cb = 0, fl = 0;
+        for (int g = 0; g < S.n; g++) {
+            const bool in = k >= S.c[g].chunk_begin;
+            base = in ? S.c[g].base : base;
+            w = in ? S.c[g].width : w;
+            lo = in ? S.c[g].lds_off : lo;
+            cb = in ? S.c[g].chunk_begin : cb;
+            fl = in ? S.c[g].flags : fl;
+        }
+        const uint32_t byte = (k - cb) * 16u;
+        src[u] = base + byte;
+        step[u] = w * T;
+        dst[u] = lo + byte;
+        okm |= (k < (uint32_t)P.total_chunks ? 1u : 0u) << u;
+        boolm |= (fl & 1u) << u;
+    }
+    u32x4 v[kStageSlots];
+    auto issue = [&](uint64_t t) {
+#pragma unroll
+        for (int u = 0; u < kStageSlots; u++)
+            if (okm & (1u << u)) v[u] = gload16<false>(src[u] + t * (uint64_t)step[u]);
+    };
+    uint64_t tile = blockIdx.x;
+    if (tile < nfull) issue(tile);
+
+    // ---- per-thread dword descriptor (segments padded to MAXSEG: mask 0)
+    uint32_t X0[MAXSEG], xs[MAXSEG], xm[MAXSEG], cval = 0;
+#pragma unroll
+    for (int g = 0; g < MAXSEG; g++) { X0[g] = 0; xs[g] = 0; xm[g] = 0; }
+    if (s < R) {
+        const DwDesc* dd = P.dw + q;
+        cval = dd->cval;
+        const uint32_t ns = dd->nseg;
+#pragma unroll
+        for (int g = 0; g < MAXSEG; g++) {
+            if ((uint32_t)g < ns) {
+                const DwSeg sg = dd->seg[g];
+                X0[g] = (uint32_t)sg.a + s * sg.w;
+                xs[g] = R * sg.w;
+                xm[g] = sg.mask;
+            }
+        }
+    }
+
+    const uint32_t* l32 = (const uint32_t*)lds;
+    for (; tile < nfull; tile += gridDim.x) {
+        __syncthreads();  // the previous tile's LDS reads are done
+#pragma unroll
+        for (int u = 0; u < kStageSlots; u++) {
+            if (okm & (1u << u)) {
+                u32x4 x = v[u];
+                if (boolm & (1u << u)) {
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        uint32_t t = x[e] | (x[e] >> 4);
+                        t |= t >> 2;
+                        t |= t >> 1;
+                        x[e] = t & 0x01010101u;
+                    }
+                }
+                *(u32x4*)(lds + dst[u]) = x;
+            }
+        }
+        __syncthreads();
+        const uint64_t nxt = tile + gridDim.x;
+        if (nxt < nfull) issue(nxt);
+        if (s < R) {
+            uint32_t* o32 = (uint32_t*)(out + tile * (uint64_t)T * B) + s * Q4 + q;
+            uint32_t X[MAXSEG];
+#pragma unroll
+            for (int g = 0; g < MAXSEG; g++) X[g] = X0[g];
+            auto one = [&]() {
+                uint32_t val = cval;
+#pragma unroll
+                for (int g = 0; g < MAXSEG; g++) {
+                    const uint32_t a = X[g];
+                    const uint32_t lo = l32[a >> 2], hi = l32[(a >> 2) + 1];
+                    val |= __builtin_amdgcn_alignbyte(hi, lo, a) & xm[g];
+                    X[g] += xs[g];
+                }
+                __builtin_nontemporal_store(val, o32);
+                o32 += R * Q4;
+            };
+            if (PER > 0) {
+#pragma unroll 4
+                for (int it = 0; it < PER; it++) one();
+            } else {
+                for (uint32_t j = s; j < T; j += R) one();
+            }
+        }
+        if (status)
+            for (uint32_t i = tid; i < T; i += kBlock) status[tile * T + i] = st_val;
+    }
+
+    // ---- partial last tile
+    if (n > nfull * T && blockIdx.x == (uint32_t)(nfull % gridDim.x)) {
+        LFix* l = (LFix*)(lds + P.fc_lds);
+        __syncthreads();
+        for (int g = threadIdx.x; g < S.n; g += kBlock)
+            l[g] = LFix{S.c[g].base, S.c[g].width, S.c[g].lds_off, S.c[g].chunk_begin, 0};
+        __syncthreads();
+        const uint64_t blob0 = nfull * T;
+        const uint32_t rows = (uint32_t)(n - blob0);
+        stage_tile<false>(P, cols, lds, blob0, rows, T);
+        __syncthreads();
+        if (s < R) {
+            const DwDesc* d = P.dw + q;
+            const uint32_t ns = d->nseg, cv = d->cval;
+            uint32_t* o32 = (uint32_t*)(out + blob0 * (uint64_t)B) + q;
+            for (uint32_t j = s; j < rows; j += R) {
+                uint32_t val = cv;
+                for (uint32_t g = 0; g < ns; g++) {
+                    const DwSeg sg = d->seg[g];
+                    uint32_t x = lds_dword_at(l32, (uint32_t)sg.a + j * sg.w) & sg.mask;
+                    if (sg.flags & 1u) x = x ? (sg.mask & 0x01010101u) : 0u;
+                    val |= x;
+                }
+                o32[(uint64_t)j * Q4] = val;
+            }
+        }
+        if (status)
+            for (uint32_t i = tid; i < rows; i += kBlock) status[blob0 + i] = st_val;
+    }
+}
+
 // Lane-invariant form with the output tile re-staged in LDS so HBM sees only
 // 16-B-per-lane stores: dwords are built into registers (<= 16 per thread,
 // T*B <= 16 KiB), the input tile is retired by a barrier, the block writes the
@@ -2011,7 +2171,10 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
             if (flags & PACKOS_ENC_FORCE_GENERIC) variant = 8;
             const bool dw_ok = !s->fdw.empty();
             const bool dw16_ok = dw_ok && (uint64_t)s->fix_T * B <= 16 * 1024;
-            if (variant == 0) variant = dw_ok ? kDefaultFixedVariant : 8;
+            const bool pipe_ok = dw_ok && (int)s->fcols.size() <= kStageCols && s->fix_maxseg >= 1 &&
+                                 s->fix_maxseg <= 4 && (uint64_t)s->fix_T * B <= 16 * 1024;
+            if (variant == 0) variant = pipe_ok ? 14 : dw_ok ? kDefaultFixedVariant : 8;
+            if (variant == 14 && !pipe_ok) variant = dw_ok ? kDefaultFixedVariant : 8;
             if ((variant >= 5 && variant <= 7 && !dw16_ok) || ((variant <= 4 || variant >= 9) && !dw_ok)) variant = 8;
             const dim3 g((unsigned)tiles), b(kBlock);
             const size_t fcb = ((s->fcols.size() * kLFixBytes) + 15) / 16 * 16;
@@ -2042,6 +2205,41 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
                 case 11: hipLaunchKernelGGL((k_encode_fixed_dw<false, true, false, 2>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
                 case 12: hipLaunchKernelGGL((k_encode_fixed_dw<true, true, false, 2>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
                 case 13: hipLaunchKernelGGL((k_encode_fixed_dw<false, true, false, 4>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
+                case 14: {
+                    FixStage S;
+                    memset(&S, 0, sizeof(S));
+                    S.n = (int32_t)s->fcols.size();
+                    for (int k = 0; k < S.n; k++) {
+                        const FixCol& fc = s->fcols[k];
+                        S.c[k] = FixStageCol{ec.data[fc.col], fc.width, fc.lds_off, fc.chunk_begin, fc.flags};
+                    }
+                    const uint64_t full = n / s->fix_T;
+                    const int per = (kBlock / (int)(B / 4)) * 16 == s->fix_T ? 16 : 0;
+                    // persistent grid: exactly the resident workgroups (a grid
+                    // larger than one wave of residency leaves a tail)
+                    auto grid_of = [&](const void* fn) {
+                        int occ = 0;
+                        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kBlock, lds_dw) != hipSuccess || occ < 1)
+                            occ = 1;
+                        if (const char* e = getenv("PACKOS_PIPE_WGS")) occ = std::max(1, std::min(occ, atoi(e)));
+                        return dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(full, (uint64_t)cu_count(dev) * occ)));
+                    };
+#define PIPE(MS, PER)                                                                                      \
+    hipLaunchKernelGGL((k_encode_fixed_pipe<MS, PER>), grid_of((const void*)k_encode_fixed_pipe<MS, PER>), b, \
+                       lds_dw, st, pdw, S, ec, out, (uint64_t)n, status, stv)
+                    switch (s->fix_maxseg * 2 + (per ? 1 : 0)) {
+                        case 2: PIPE(1, 0); break;
+                        case 3: PIPE(1, 16); break;
+                        case 4: PIPE(2, 0); break;
+                        case 5: PIPE(2, 16); break;
+                        case 6: PIPE(3, 0); break;
+                        case 7: PIPE(3, 16); break;
+                        case 8: PIPE(4, 0); break;
+                        default: PIPE(4, 16); break;
+                    }
+#undef PIPE
+                    break;
+                }
                 default: variant = 8; break;
             }
             if (variant == 8) {

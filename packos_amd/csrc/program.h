@@ -82,6 +82,7 @@ struct FixCol {
     uint32_t width;      // row width in bytes
     uint32_t lds_off;    // LDS offset of this column's tile region
     uint32_t chunk_begin;// first 16-byte chunk of this column within the tile
+    uint32_t flags;      // bit0: bool column (any non-zero byte encodes as 1)
 };
 
 // Lane-invariant form (B % 4 == 0): thread t always builds output dword
@@ -107,6 +108,23 @@ struct FixProgram {
     const DwDesc* dw;            // B/4 entries when B % 4 == 0
     int32_t B, T, n_fcols, lds_bytes, total_chunks, overflow;
     int32_t fc_lds;              // LDS offset of the per-launch copy of fcols (set at launch)
+};
+
+// Staging plan of the pipelined fixed-layout kernel, passed BY VALUE as a
+// kernel argument so a workgroup can issue its first tile's loads straight
+// from kernarg (no dependent global table read in front of them).
+constexpr int kStageCols = 16;
+struct FixStageCol {
+    const uint8_t* base;   // column data pointer (row 0)
+    uint32_t width;        // row bytes
+    uint32_t lds_off;      // LDS offset of the column's tile region
+    uint32_t chunk_begin;  // first 16-B chunk of the column within a tile
+    uint32_t flags;        // bit0: bool column
+};
+struct FixStage {
+    FixStageCol c[kStageCols];
+    int32_t n;
+    int32_t pad;
 };
 
 // ---------------------------------------------------------------- decode ----

@@ -61,6 +61,7 @@ struct packos_schema {
     std::vector<packos::FixCol> fcols;
     std::vector<packos::DwDesc> fdw;   // lane-invariant descriptors (B % 4 == 0)
     int fix_T = 0, fix_lds = 0, fix_chunks = 0;
+    int fix_maxseg = 0;                 // max column segments of any output dword (fdw)
 
     // decode program
     std::vector<packos::DecNode> dnodes;
