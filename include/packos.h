@@ -210,9 +210,11 @@ int packos_encoded_size_batch(const packos_schema* s, const packos_column* cols,
  * the one-wavefront-per-blob kernel instead of the tiled one                 */
 #define PACKOS_ENC_FORCE_GENERIC 2u
 /* testing/benchmark knob: pick the fixed-layout kernel variant (0 = auto):
- * 1..4 lane-invariant, dword stores {plain, NT stores, NT loads, NT both};
- * 5..7 lane-invariant, LDS re-staged 16-B stores {plain, NT stores, NT both};
- * 8 general 4-blob-period kernel                                             */
+ * 13 one tile per workgroup, LDS-DMA staging, single-source dwords (auto
+ *    when B % 4 == 0, 16 <= B <= 1024, <= 16 fixed columns);
+ * 1, 2 lane-invariant dword kernel {plain, NT stores} (auto otherwise when
+ *    B % 4 == 0; also the partial last tile of variant 13);
+ * 8 general 4-blob-period kernel (any B)                                     */
 #define PACKOS_ENC_FIXED_VARIANT(v) (((uint32_t)(v) & 0xFu) << 4)
 int packos_encode_batch(const packos_schema* s, const packos_column* cols, size_t n_blobs,
                         uint8_t* out_arena, uint64_t out_capacity, uint64_t* out_offsets,

@@ -10,12 +10,17 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpackos.so")
+LIB_PATH = os.environ.get("PACKOS_LIB") or os.path.join(HERE, "libpackos.so")  # override: experiments only
 
 MODE_PUTACCESS = 0
 MODE_PACKABLE = 1
 ENC_OFFSETS_READY = 1
 ENC_FORCE_GENERIC = 2
+
+
+def ENC_FIXED_VARIANT(v: int) -> int:
+    """PACKOS_ENC_FIXED_VARIANT(v): testing/benchmark knob (include/packos.h)."""
+    return (v & 0xF) << 4
 
 STATUS_PANIC = 0x40000000
 STATUS_OVERFLOW13 = 0x80000000

@@ -400,11 +400,12 @@ struct Builder {
             lds_of_col[c] = (int)lds;
             uint32_t bytes = (uint32_t)T * fc.width;
             chunks += bytes / 16;
-            lds += bytes + 32;  // region + guard (next region's leading guard)
-            lds = (lds + 15) & ~15u;
+            lds += bytes;  // regions back to back in chunk order (T*w % 16 == 0): chunk k
+                           // of a tile sits at 16 + 16k, the layout one LDS-DMA wave
+                           // instruction (1 KiB, lane-linear) fills
             s->fcols.push_back(fc);
         }
-        s->fix_lds = (int)lds + 16;
+        s->fix_lds = (int)lds + 32;  // tail guard (read-past of the last region, dummy slot)
         s->fix_chunks = (int)chunks;
         // decode fast path tables: per-dword constant check, per-column
         // blob offset, canonical blob (payload bytes zero)
@@ -515,6 +516,53 @@ struct Builder {
                 }
                 s->fdw.push_back(dd);
                 s->fix_maxseg = std::max<int>(s->fix_maxseg, (int)dd.nseg);
+            }
+            // single-source form for k_encode_fixed_tile: X dwords (several
+            // runs, or a bool byte to normalise) get a slot in the X region
+            s->ftdw = s->fdw;
+            s->fxdw.clear();
+            s->fxq.clear();
+            for (int64_t q = 0; q < B / 4; q++) {
+                const DwDesc& d = s->fdw[q];
+                bool x = d.nseg > 1;
+                for (uint32_t g = 0; g < d.nseg; g++) x = x || (d.seg[g].flags & 1u);
+                if (x) { s->fxq.push_back((uint32_t)q); s->fxdw.push_back(d); }
+            }
+            const uint32_t nx = (uint32_t)s->fxq.size();
+            s->fix_x_lds = (s->fix_lds + 15) / 16 * 16;
+            s->fix_tile_lds = s->fix_x_lds + (int)(T * nx * 4) + 16;
+            for (uint32_t k = 0; k < nx; k++) {
+                DwDesc& t = s->ftdw[s->fxq[k]];
+                uint32_t cm = 0;
+                for (uint32_t g = 0; g < t.nseg; g++) cm |= t.seg[g].mask;
+                DwSeg sg{};
+                sg.a = s->fix_x_lds + (int32_t)(4 * k);
+                sg.w = 4 * nx;
+                sg.mask = cm;
+                sg.flags = 0;
+                t.seg[0] = sg;
+                for (int g = 1; g < 4; g++) t.seg[g] = DwSeg{};
+                t.nseg = 1;
+            }
+            // a constant-only dword still issues the (masked) LDS read in the
+            // branch-free kernels: point it at a source another lane of the
+            // same 32-lane LDS group reads, so it broadcasts instead of
+            // adding a bank conflict
+            const int64_t Q4 = B / 4;
+            for (int64_t q = 0; q < Q4; q++) {
+                if (s->fdw[q].nseg) continue;
+                int64_t best = -1;
+                for (int64_t d = 1; d < Q4 && best < 0; d++)
+                    for (int64_t c : {q + d, q - d})
+                        if (c >= 0 && c < Q4 && c / 32 == q / 32 && s->fdw[c].nseg && best < 0) best = c;
+                if (best >= 0) {
+                    s->fdw[q].seg[0] = s->fdw[best].seg[0];
+                    s->fdw[q].seg[0].mask = 0;
+                    s->fdw[q].seg[0].flags = 0;
+                    s->ftdw[q].seg[0] = s->ftdw[best].seg[0];
+                    s->ftdw[q].seg[0].mask = 0;
+                    s->ftdw[q].seg[0].flags = 0;
+                }
             }
         }
         // tile + descriptor tables must fit the 64 KiB dynamic LDS of one launch

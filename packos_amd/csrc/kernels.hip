@@ -155,9 +155,8 @@ __device__ __forceinline__ uint32_t lds_dword_at(const uint32_t* l32, uint32_t a
 
 // Lane-invariant form (B % 4 == 0): thread t owns output dword q = t % (B/4)
 // of blobs s, s+R, s+2R ... of the tile; its byte sources sit in registers.
-// PERSIST: a grid of ~CUs x 8 workgroups walks the tiles (descriptors loaded
-// once per workgroup instead of once per tile).
-template <bool NTL, bool NTS, bool PERSIST = false, int U = 1>
+// Used for partial last tiles and shapes k_encode_fixed_tile does not take.
+template <bool NTS>
 __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCols cols, uint8_t* __restrict__ out,
                                                             uint64_t n, uint32_t* __restrict__ status,
                                                             uint32_t st_val) {
@@ -166,240 +165,19 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCol
     const uint32_t Q4 = (uint32_t)P.B >> 2;
     const uint32_t tid = threadIdx.x;
     const uint32_t q = tid % Q4, s = tid / Q4, R = kBlock / Q4;
-    const uint64_t ntiles = (n + T - 1) / T;
-    DwDesc d;
-    if (s < R) d = P.dw[q];
-    fcols_to_lds(P, cols, lds);
-    __syncthreads();
-    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += PERSIST ? gridDim.x : ntiles) {
-        const uint64_t blob0 = tile * (uint64_t)T;
-        const uint32_t rows = (uint32_t)min((uint64_t)T, n - blob0);
-        if (PERSIST && tile != blockIdx.x) __syncthreads();  // previous tile's LDS reads are done
-        stage_tile<NTL>(P, cols, lds, blob0, rows, (uint32_t)T);
-        __syncthreads();
-        if (s < R) {
-            const uint32_t* l32 = (const uint32_t*)lds;
-            uint32_t* o32 = (uint32_t*)(out + blob0 * (uint64_t)P.B) + q;
-            // U blobs per iteration: their LDS reads issue back to back
-            for (uint32_t j = s; j < rows; j += U * R) {
-                uint32_t v[U];
-#pragma unroll
-                for (int uu = 0; uu < U; uu++) {
-                    const uint32_t jj = j + uu * R;
-                    v[uu] = d.cval;
-#pragma unroll
-                    for (int g = 0; g < 4; g++) {
-                        if ((uint32_t)g < d.nseg) {
-                            uint32_t x = lds_dword_at(l32, (uint32_t)d.seg[g].a + jj * d.seg[g].w) & d.seg[g].mask;
-                            if (d.seg[g].flags & 1u) x = x ? (d.seg[g].mask & 0x01010101u) : 0u;
-                            v[uu] |= x;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int uu = 0; uu < U; uu++) {
-                    const uint32_t jj = j + uu * R;
-                    if (jj < rows) {
-                        if (NTS) __builtin_nontemporal_store(v[uu], o32 + (uint64_t)jj * Q4);
-                        else o32[(uint64_t)jj * Q4] = v[uu];
-                    }
-                }
-            }
-        }
-        if (status)
-            for (uint32_t i = tid; i < rows; i += kBlock) status[blob0 + i] = st_val;
-    }
-}
-
-// Pipelined lane-invariant form (default for fixed schemas with B % 4 == 0).
-// A grid of ~CUs x 8 workgroups walks the full tiles (tile = blockIdx.x,
-// + gridDim.x, ...).  Per tile: the input registers fetched during the
-// previous tile's assembly go to LDS (bool columns normalised to 0/1 here, so
-// assembly needs no per-segment flag test), the NEXT tile's loads are issued,
-// then each thread builds its output dwords from LDS (<= MAXSEG sources, all
-// padded to MAXSEG so the inner loop is branch-free) and stores them NT.  So
-// every workgroup keeps a tile of loads in flight while it assembles and
-// stores, and the staging plan (which column chunk each of a thread's 4 slots
-// fetches; from kernarg, no dependent table read before the first loads) and
-// the dword descriptors are set up once per workgroup, not once per tile.
-// The partial last tile (n % T blobs) goes through stage_tile + the flagged
-// dword loop of k_encode_fixed_dw in the workgroup that would own it.
-// Measured against k_encode_fixed_dw: PMC showed ~790 VALU per wave per tile
-// there (column walk + 4-way flagged segment loop), the bulk of the kernel.
-template <int MAXSEG, int PER>
-__global__ __launch_bounds__(kBlock) void k_encode_fixed_pipe(FixProgram P, FixStage S, EncCols cols,
-                                                              uint8_t* __restrict__ out, uint64_t n,
-                                                              uint32_t* __restrict__ status, uint32_t st_val) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const uint32_t T = (uint32_t)P.T;
-    const uint32_t B = (uint32_t)P.B;
-    const uint32_t Q4 = B >> 2;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t q = tid % Q4, s = tid / Q4, R = kBlock / Q4;
-    const uint64_t nfull = n / T;
-
-    // ---- staging plan: slot u of this thread = chunk u*256 + tid of a tile
-    const uint8_t* src[kStageSlots];
-    uint32_t step[kStageSlots], dst[kStageSlots];
-    uint32_t okm = 0, boolm = 0;
-#pragma unroll
-    for (int u = 0; u < kStageSlots; u++) {
-        const uint32_t k = (uint32_t)u * kBlock + tid;
-        const uint8_t* base = nullptr;
-        uint32_t w = 0, lo = 0, cb = 0, fl = 0;
-        for (int g = 0; g < S.n; g++) {
-            const bool in = k >= S.c[g].chunk_begin;
-            base = in ? S.c[g].base : base;
-            w = in ? S.c[g].width : w;
-            lo = in ? S.c[g].lds_off : lo;
-            cb = in ? S.c[g].chunk_begin : cb;
-            fl = in ? S.c[g].flags : fl;
-        }
-        const uint32_t byte = (k - cb) * 16u;
-        src[u] = base + byte;
-        step[u] = w * T;
-        dst[u] = lo + byte;
-        okm |= (k < (uint32_t)P.total_chunks ? 1u : 0u) << u;
-        boolm |= (fl & 1u) << u;
-    }
-    u32x4 v[kStageSlots];
-    auto issue = [&](uint64_t t) {
-#pragma unroll
-        for (int u = 0; u < kStageSlots; u++)
-            if (okm & (1u << u)) v[u] = gload16<false>(src[u] + t * (uint64_t)step[u]);
-    };
-    uint64_t tile = blockIdx.x;
-    if (tile < nfull) issue(tile);
-
-    // ---- per-thread dword descriptor (segments padded to MAXSEG: mask 0)
-    uint32_t X0[MAXSEG], xs[MAXSEG], xm[MAXSEG], cval = 0;
-#pragma unroll
-    for (int g = 0; g < MAXSEG; g++) { X0[g] = 0; xs[g] = 0; xm[g] = 0; }
-    if (s < R) {
-        const DwDesc* dd = P.dw + q;
-        cval = dd->cval;
-        const uint32_t ns = dd->nseg;
-#pragma unroll
-        for (int g = 0; g < MAXSEG; g++) {
-            if ((uint32_t)g < ns) {
-                const DwSeg sg = dd->seg[g];
-                X0[g] = (uint32_t)sg.a + s * sg.w;
-                xs[g] = R * sg.w;
-                xm[g] = sg.mask;
-            }
-        }
-    }
-
-    const uint32_t* l32 = (const uint32_t*)lds;
-    for (; tile < nfull; tile += gridDim.x) {
-        __syncthreads();  // the previous tile's LDS reads are done
-#pragma unroll
-        for (int u = 0; u < kStageSlots; u++) {
-            if (okm & (1u << u)) {
-                u32x4 x = v[u];
-                if (boolm & (1u << u)) {
-#pragma unroll
-                    for (int e = 0; e < 4; e++) {
-                        uint32_t t = x[e] | (x[e] >> 4);
-                        t |= t >> 2;
-                        t |= t >> 1;
-                        x[e] = t & 0x01010101u;
-                    }
-                }
-                *(u32x4*)(lds + dst[u]) = x;
-            }
-        }
-        __syncthreads();
-        const uint64_t nxt = tile + gridDim.x;
-        if (nxt < nfull) issue(nxt);
-        if (s < R) {
-            uint32_t* o32 = (uint32_t*)(out + tile * (uint64_t)T * B) + s * Q4 + q;
-            uint32_t X[MAXSEG];
-#pragma unroll
-            for (int g = 0; g < MAXSEG; g++) X[g] = X0[g];
-            auto one = [&]() {
-                uint32_t val = cval;
-#pragma unroll
-                for (int g = 0; g < MAXSEG; g++) {
-                    const uint32_t a = X[g];
-                    const uint32_t lo = l32[a >> 2], hi = l32[(a >> 2) + 1];
-                    val |= __builtin_amdgcn_alignbyte(hi, lo, a) & xm[g];
-                    X[g] += xs[g];
-                }
-                __builtin_nontemporal_store(val, o32);
-                o32 += R * Q4;
-            };
-            if (PER > 0) {
-#pragma unroll 4
-                for (int it = 0; it < PER; it++) one();
-            } else {
-                for (uint32_t j = s; j < T; j += R) one();
-            }
-        }
-        if (status)
-            for (uint32_t i = tid; i < T; i += kBlock) status[tile * T + i] = st_val;
-    }
-
-    // ---- partial last tile
-    if (n > nfull * T && blockIdx.x == (uint32_t)(nfull % gridDim.x)) {
-        LFix* l = (LFix*)(lds + P.fc_lds);
-        __syncthreads();
-        for (int g = threadIdx.x; g < S.n; g += kBlock)
-            l[g] = LFix{S.c[g].base, S.c[g].width, S.c[g].lds_off, S.c[g].chunk_begin, 0};
-        __syncthreads();
-        const uint64_t blob0 = nfull * T;
-        const uint32_t rows = (uint32_t)(n - blob0);
-        stage_tile<false>(P, cols, lds, blob0, rows, T);
-        __syncthreads();
-        if (s < R) {
-            const DwDesc* d = P.dw + q;
-            const uint32_t ns = d->nseg, cv = d->cval;
-            uint32_t* o32 = (uint32_t*)(out + blob0 * (uint64_t)B) + q;
-            for (uint32_t j = s; j < rows; j += R) {
-                uint32_t val = cv;
-                for (uint32_t g = 0; g < ns; g++) {
-                    const DwSeg sg = d->seg[g];
-                    uint32_t x = lds_dword_at(l32, (uint32_t)sg.a + j * sg.w) & sg.mask;
-                    if (sg.flags & 1u) x = x ? (sg.mask & 0x01010101u) : 0u;
-                    val |= x;
-                }
-                o32[(uint64_t)j * Q4] = val;
-            }
-        }
-        if (status)
-            for (uint32_t i = tid; i < rows; i += kBlock) status[blob0 + i] = st_val;
-    }
-}
-
-// Lane-invariant form with the output tile re-staged in LDS so HBM sees only
-// 16-B-per-lane stores: dwords are built into registers (<= 16 per thread,
-// T*B <= 16 KiB), the input tile is retired by a barrier, the block writes the
-// output tile over it, then copies it out with global_store_dwordx4.
-template <bool NTL, bool NT>
-__global__ __launch_bounds__(kBlock) void k_encode_fixed_dw16(FixProgram P, EncCols cols, uint8_t* __restrict__ out,
-                                                              uint64_t n, uint32_t* __restrict__ status,
-                                                              uint32_t st_val) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    constexpr int kMaxPer = 16;
-    const int T = P.T;
-    const uint32_t Q4 = (uint32_t)P.B >> 2;
     const uint64_t blob0 = (uint64_t)blockIdx.x * (uint64_t)T;
     const uint32_t rows = (uint32_t)min((uint64_t)T, n - blob0);
-    const uint32_t tid = threadIdx.x;
-    const uint32_t q = tid % Q4, s = tid / Q4, R = kBlock / Q4;
     DwDesc d;
     if (s < R) d = P.dw[q];
     fcols_to_lds(P, cols, lds);
     __syncthreads();
-    stage_tile<NTL>(P, cols, lds, blob0, rows, (uint32_t)T);
+    stage_tile<false>(P, cols, lds, blob0, rows, (uint32_t)T);
     __syncthreads();
-    uint32_t vals[kMaxPer];
-    const uint32_t* l32 = (const uint32_t*)lds;
-#pragma unroll
-    for (int m = 0; m < kMaxPer; m++) {
-        const uint32_t j = s + (uint32_t)m * R;
-        uint32_t v = d.cval;
-        if (s < R && j < rows) {
+    if (s < R) {
+        const uint32_t* l32 = (const uint32_t*)lds;
+        uint32_t* o32 = (uint32_t*)(out + blob0 * (uint64_t)P.B) + q;
+        for (uint32_t j = s; j < rows; j += R) {
+            uint32_t v = d.cval;
 #pragma unroll
             for (int g = 0; g < 4; g++) {
                 if ((uint32_t)g < d.nseg) {
@@ -408,31 +186,114 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw16(FixProgram P, EncC
                     v |= x;
                 }
             }
-        }
-        vals[m] = v;
-    }
-    __syncthreads();
-    uint32_t* o_lds = (uint32_t*)lds;
-#pragma unroll
-    for (int m = 0; m < kMaxPer; m++) {
-        const uint32_t j = s + (uint32_t)m * R;
-        if (s < R && j < rows) o_lds[j * Q4 + q] = vals[m];
-    }
-    __syncthreads();
-    const uint32_t tile_bytes = rows * (uint32_t)P.B;
-    uint8_t* obase = out + blob0 * (uint64_t)P.B;
-    for (uint32_t c = tid; c * 16 < tile_bytes; c += kBlock) {
-        const uint32_t ob = 16 * c;
-        if (ob + 16 <= tile_bytes) {
-            const u32x4 v = *(const u32x4*)(lds + ob);
-            if (NT) __builtin_nontemporal_store(v, (u32x4*)(obase + ob));
-            else *(u32x4*)(obase + ob) = v;
-        } else {
-            for (uint32_t jb = ob; jb < tile_bytes; jb++) obase[jb] = lds[jb];
+            if (NTS) __builtin_nontemporal_store(v, o32 + (uint64_t)j * Q4);
+            else o32[(uint64_t)j * Q4] = v;
         }
     }
     if (status)
         for (uint32_t i = tid; i < rows; i += kBlock) status[blob0 + i] = st_val;
+}
+
+// One 16-B-per-lane LDS-DMA load: lane l's 16 bytes land at LDS byte address
+// m0 + 16*l (wave-uniform m0).  Written as asm so the compiler neither waits
+// for it (it would drain with vmcnt(0) before every LDS read or barrier) nor
+// reorders LDS accesses across it: every wait for it is explicit.
+__device__ __forceinline__ void dma16(const uint8_t* gsrc, uint32_t lds_addr) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_addr)
+                 : "memory");
+}
+
+// One tile per workgroup, LDS-DMA staging with a wave-uniform column walk.
+// Each wave-instruction fetches 64 consecutive 16-B chunks of ONE column
+// (column base + tile offset are scalars, so a load costs ~2 VALU; no per-
+// lane column search), straight into that column's LDS region.  Then one
+// vmcnt(0) + barrier.  Output dwords fed by more than one column run or by a
+// bool byte ("X dwords", 3 of 64 for metric M) are assembled once per blob
+// into an LDS X region (bools normalised there) + barrier, so in the main
+// assembly EVERY dword has exactly one source: one ds_read2_b32 +
+// v_alignbyte + v_and_or per output dword, 1-KiB-strided NT dword stores.
+// (A branch-free per-lane segment loop padded to the widest dword doubled the
+// LDS reads and their bank conflicts.)  No persistent loop: the workgroup
+// exits without waiting for its stores, so every resident workgroup spends
+// its life with loads or stores in flight (the shape of the fastest plain
+// copy of this traffic, tools/membench2.hip).
+template <int PER>  // T == PER * R (the compiler's T = 16 * floor(1024 / B))
+__global__ __launch_bounds__(kBlock) void k_encode_fixed_tile(FixProgram P, FixStage S, uint8_t* __restrict__ out,
+                                                              uint32_t* __restrict__ status, uint32_t st_val) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t T = (uint32_t)P.T;
+    const uint32_t B = (uint32_t)P.B;
+    const uint32_t Q4 = B >> 2;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t q = tid % Q4, s = tid / Q4, R = kBlock / Q4;
+    const uint32_t lane = tid % kWave, wv = tid / kWave;
+    const uint64_t blob0 = blockIdx.x * (uint64_t)T;  // full tiles only (the launcher sends
+                                                      // a partial last tile to k_encode_fixed_dw)
+#ifndef ENC_ABL
+#define ENC_ABL 0
+#endif
+    const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+    for (int g = 0; g < (ENC_ABL == 2 ? 0 : S.n); g++) {
+        const uint32_t nch = (T * S.c[g].width) >> 4;
+        const uint8_t* cbase = S.c[g].base + blob0 * S.c[g].width;
+        for (uint32_t c0 = wv * kWave; c0 < nch; c0 += kBlock) {
+            if (c0 + lane < nch)
+                dma16(cbase + (c0 + lane) * 16u, __builtin_amdgcn_readfirstlane(lds0 + S.c[g].lds_off + c0 * 16u));
+        }
+    }
+    // descriptors (their global loads queue behind the DMA)
+    const DwDesc* dd = P.tdw + q;
+    const uint32_t cval = dd->cval;
+    const DwSeg sg = dd->seg[0];
+    uint32_t a = (uint32_t)sg.a + s * sg.w;  // LDS byte address of this thread's first dword
+    const uint32_t xs = R * sg.w, xm = sg.mask;
+    const uint32_t nxi = T * (uint32_t)P.nx;
+    DwDesc xd;  // this thread's first X item
+    if (tid < nxi) xd = P.xdw[tid % (uint32_t)P.nx];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    uint32_t* l32 = (uint32_t*)lds;
+    if (nxi && ENC_ABL != 3) {
+        auto assemble = [&](uint32_t i, const DwDesc& d) {
+            const uint32_t j = i / (uint32_t)P.nx;
+            uint32_t val = 0;
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                if ((uint32_t)g < d.nseg) {
+                    uint32_t x = lds_dword_at(l32, (uint32_t)d.seg[g].a + j * d.seg[g].w) & d.seg[g].mask;
+                    if (d.seg[g].flags & 1u) x = x ? (d.seg[g].mask & 0x01010101u) : 0u;
+                    val |= x;
+                }
+            }
+            l32[((uint32_t)P.x_lds >> 2) + i] = val;
+        };
+        if (tid < nxi) assemble(tid, xd);
+        for (uint32_t i = tid + kBlock; i < nxi; i += kBlock) assemble(i, P.xdw[i % (uint32_t)P.nx]);
+        __syncthreads();
+    }
+    if (s < R) {  // R * Q4 <= 256: the rest of the threads idle here
+        uint32_t* o32 = (uint32_t*)(out + blob0 * B) + s * Q4 + q;
+        const uint32_t ostep = R * Q4;
+#pragma unroll
+        for (int it = 0; it < PER; it++) {
+            uint32_t val = cval;
+            if (ENC_ABL != 1) {
+                const uint32_t lo = l32[a >> 2], hi = l32[(a >> 2) + 1];
+                val |= __builtin_amdgcn_alignbyte(hi, lo, a) & xm;  // uses a & 3
+            } else {
+                val ^= a * 0x9E3779B1u + (uint32_t)blob0;  // ablation: data-dependent, no LDS read
+            }
+            a += xs;
+            if (it & 1) asm volatile("" : "+v"(a));  // two iterations' reads in flight, no address table
+            __builtin_nontemporal_store(val, o32);
+            o32 += ostep;
+        }
+    }
+    if (status)
+        for (uint32_t i = tid; i < T; i += kBlock) status[blob0 + i] = st_val;
 }
 
 // General form (any B <= 1024): 16-B output chunks, per-dword segment lists
@@ -1928,16 +1789,6 @@ int current_device(int* dev) {
     return PACKOS_OK;
 }
 
-int cu_count(int dev) {
-    static int cache[64] = {0};
-    if (dev < 0 || dev >= 64) return 256;
-    if (!cache[dev]) {
-        int v = 0;
-        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-        cache[dev] = v;
-    }
-    return cache[dev];
-}
 
 // Does the all-present blob of a fixed schema decode cleanly?  Runs the same
 // decode_blob the device runs, on the host, over the canonical blob (zero
@@ -2014,6 +1865,9 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     size_t o_fidx = put_bytes(blob, s->fseg_index);
     size_t o_fcols = put_bytes(blob, s->fcols);
     size_t o_fdw = put_bytes(blob, s->fdw);
+    size_t o_ftdw = put_bytes(blob, s->ftdw);
+    size_t o_fxdw = put_bytes(blob, s->fxdw);
+    size_t o_fxq = put_bytes(blob, s->fxq);
     size_t o_dnodes = put_bytes(blob, s->dnodes);
     size_t o_dkids = put_bytes(blob, s->dkids);
     size_t o_dfix = put_bytes(blob, s->dfix);
@@ -2038,6 +1892,11 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     t.fix.seg_index = (const uint32_t*)(b + o_fidx);
     t.fix.fcols = (const FixCol*)(b + o_fcols);
     t.fix.dw = (const DwDesc*)(b + o_fdw);
+    t.fix.tdw = (const DwDesc*)(b + o_ftdw);
+    t.fix.xdw = (const DwDesc*)(b + o_fxdw);
+    t.fix.xq = (const uint32_t*)(b + o_fxq);
+    t.fix.nx = (int32_t)s->fxq.size();
+    t.fix.x_lds = s->fix_x_lds;
     t.fix.B = (int)s->all_present_size;
     t.fix.T = s->fix_T;
     t.fix.n_fcols = (int)s->fcols.size();
@@ -2167,77 +2026,47 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
         if (s->fix_ok && B >= 4 && aligned) {
             const uint64_t tiles = (n + s->fix_T - 1) / s->fix_T;
             const uint32_t stv = s->all_present_overflow ? PACKOS_STATUS_OVERFLOW13 : 0u;
+            // variant: 13 one-tile-per-workgroup LDS-DMA kernel (default where it
+            // applies), 2 lane-invariant dword kernel, 8 general 4-blob-period kernel
             int variant = (int)((flags >> 4) & 0xF);
             if (flags & PACKOS_ENC_FORCE_GENERIC) variant = 8;
-            const bool dw_ok = !s->fdw.empty();
-            const bool dw16_ok = dw_ok && (uint64_t)s->fix_T * B <= 16 * 1024;
-            const bool pipe_ok = dw_ok && (int)s->fcols.size() <= kStageCols && s->fix_maxseg >= 1 &&
-                                 s->fix_maxseg <= 4 && (uint64_t)s->fix_T * B <= 16 * 1024;
-            if (variant == 0) variant = pipe_ok ? 14 : dw_ok ? kDefaultFixedVariant : 8;
-            if (variant == 14 && !pipe_ok) variant = dw_ok ? kDefaultFixedVariant : 8;
-            if ((variant >= 5 && variant <= 7 && !dw16_ok) || ((variant <= 4 || variant >= 9) && !dw_ok)) variant = 8;
-            const dim3 g((unsigned)tiles), b(kBlock);
+            const bool dw_ok = !s->fdw.empty() && B <= 1024;
+            const bool tile_ok = dw_ok && B >= 16 && (int)s->fcols.size() <= kStageCols &&
+                                 (uint32_t)s->fix_T == 16u * (kBlock / (uint32_t)(B / 4)) &&
+                                 s->fix_tile_lds <= 64 * 1024;
+            if (variant == 0) variant = tile_ok ? 13 : dw_ok ? kDefaultFixedVariant : 8;
+            if (variant == 13 && !tile_ok) variant = dw_ok ? kDefaultFixedVariant : 8;
+            if ((variant == 1 || variant == 2) && !dw_ok) variant = 8;
             const size_t fcb = ((s->fcols.size() * kLFixBytes) + 15) / 16 * 16;
             // each kernel gets the column table copied right after the LDS it uses
-            FixProgram pdw = t->fix, pdw16 = t->fix, pgen = t->fix;
+            FixProgram pdw = t->fix, pgen = t->fix;
             pdw.fc_lds = s->fix_lds;
-            pdw16.fc_lds = (int32_t)std::max<size_t>((size_t)s->fix_lds, (size_t)s->fix_T * B);
             const size_t gen_tables = (size_t)s->fix_lds + ((B + 1) * 4 + 15) / 16 * 16 + s->fsegs.size() * sizeof(FixSeg);
             pgen.fc_lds = (int32_t)gen_tables;
             const size_t lds_dw = (size_t)pdw.fc_lds + fcb;
-            const size_t lds_dw16 = (size_t)pdw16.fc_lds + fcb;
             switch (variant) {
-                case 1: hipLaunchKernelGGL((k_encode_fixed_dw<false, false>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
-                case 2: hipLaunchKernelGGL((k_encode_fixed_dw<false, true>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
-                case 3: hipLaunchKernelGGL((k_encode_fixed_dw<true, false>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
-                case 4: hipLaunchKernelGGL((k_encode_fixed_dw<true, true>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
-                case 5: hipLaunchKernelGGL((k_encode_fixed_dw16<false, false>), g, b, lds_dw16, st, pdw16, ec, out, (uint64_t)n, status, stv); break;
-                case 6: hipLaunchKernelGGL((k_encode_fixed_dw16<false, true>), g, b, lds_dw16, st, pdw16, ec, out, (uint64_t)n, status, stv); break;
-                case 7: hipLaunchKernelGGL((k_encode_fixed_dw16<true, true>), g, b, lds_dw16, st, pdw16, ec, out, (uint64_t)n, status, stv); break;
-                case 9: case 10: {
-                    const dim3 gp((unsigned)std::min<uint64_t>(tiles, (uint64_t)cu_count(dev) * 8));
-                    if (variant == 9)
-                        hipLaunchKernelGGL((k_encode_fixed_dw<false, true, true>), gp, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv);
-                    else
-                        hipLaunchKernelGGL((k_encode_fixed_dw<true, true, true>), gp, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv);
-                    break;
-                }
-                case 11: hipLaunchKernelGGL((k_encode_fixed_dw<false, true, false, 2>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
-                case 12: hipLaunchKernelGGL((k_encode_fixed_dw<true, true, false, 2>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
-                case 13: hipLaunchKernelGGL((k_encode_fixed_dw<false, true, false, 4>), g, b, lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
-                case 14: {
+                case 1: hipLaunchKernelGGL((k_encode_fixed_dw<false>), dim3((unsigned)tiles), dim3(kBlock), lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
+                case 2: hipLaunchKernelGGL((k_encode_fixed_dw<true>), dim3((unsigned)tiles), dim3(kBlock), lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
+                case 13: {
                     FixStage S;
                     memset(&S, 0, sizeof(S));
                     S.n = (int32_t)s->fcols.size();
                     for (int k = 0; k < S.n; k++) {
                         const FixCol& fc = s->fcols[k];
                         S.c[k] = FixStageCol{ec.data[fc.col], fc.width, fc.lds_off, fc.chunk_begin, fc.flags};
+                        S.flags |= (int32_t)(fc.flags & 1u);
                     }
-                    const uint64_t full = n / s->fix_T;
-                    const int per = (kBlock / (int)(B / 4)) * 16 == s->fix_T ? 16 : 0;
-                    // persistent grid: exactly the resident workgroups (a grid
-                    // larger than one wave of residency leaves a tail)
-                    auto grid_of = [&](const void* fn) {
-                        int occ = 0;
-                        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kBlock, lds_dw) != hipSuccess || occ < 1)
-                            occ = 1;
-                        if (const char* e = getenv("PACKOS_PIPE_WGS")) occ = std::max(1, std::min(occ, atoi(e)));
-                        return dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(full, (uint64_t)cu_count(dev) * occ)));
-                    };
-#define PIPE(MS, PER)                                                                                      \
-    hipLaunchKernelGGL((k_encode_fixed_pipe<MS, PER>), grid_of((const void*)k_encode_fixed_pipe<MS, PER>), b, \
-                       lds_dw, st, pdw, S, ec, out, (uint64_t)n, status, stv)
-                    switch (s->fix_maxseg * 2 + (per ? 1 : 0)) {
-                        case 2: PIPE(1, 0); break;
-                        case 3: PIPE(1, 16); break;
-                        case 4: PIPE(2, 0); break;
-                        case 5: PIPE(2, 16); break;
-                        case 6: PIPE(3, 0); break;
-                        case 7: PIPE(3, 16); break;
-                        case 8: PIPE(4, 0); break;
-                        default: PIPE(4, 16); break;
+                    const uint64_t full = n / s->fix_T, rem = n - full * s->fix_T;
+                    if (full)
+                        hipLaunchKernelGGL((k_encode_fixed_tile<16>), dim3((unsigned)full), dim3(kBlock),
+                                           (size_t)s->fix_tile_lds, st, pdw, S, out, status, stv);
+                    if (rem) {  // partial last tile: the lane-invariant dword kernel on the remainder
+                        const uint64_t b0 = full * s->fix_T;
+                        EncCols et = ec;
+                        for (const FixCol& fc : s->fcols) et.data[fc.col] = ec.data[fc.col] + b0 * fc.width;
+                        hipLaunchKernelGGL((k_encode_fixed_dw<true>), dim3(1), dim3(kBlock), lds_dw, st, pdw, et,
+                                           out + b0 * B, rem, status ? status + b0 : nullptr, stv);
                     }
-#undef PIPE
                     break;
                 }
                 default: variant = 8; break;

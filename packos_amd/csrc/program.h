@@ -108,6 +108,14 @@ struct FixProgram {
     const DwDesc* dw;            // B/4 entries when B % 4 == 0
     int32_t B, T, n_fcols, lds_bytes, total_chunks, overflow;
     int32_t fc_lds;              // LDS offset of the per-launch copy of fcols (set at launch)
+    // k_encode_fixed_tile: output dwords fed by >1 column run or by a bool
+    // byte ("X dwords") are assembled once per blob into an LDS X region
+    // (T rows x nx dwords at x_lds); tdw then gives every dword ONE aligned-
+    // or-shifted source (its column run, or its X slot)
+    const DwDesc* tdw;           // B/4 single-source descriptors
+    const DwDesc* xdw;           // nx full descriptors of the X dwords
+    const uint32_t* xq;          // nx: output dword index of each X dword (unused by kernels)
+    int32_t nx, x_lds;
 };
 
 // Staging plan of the pipelined fixed-layout kernel, passed BY VALUE as a
@@ -124,7 +132,7 @@ struct FixStageCol {
 struct FixStage {
     FixStageCol c[kStageCols];
     int32_t n;
-    int32_t pad;
+    int32_t flags;         // bit0: some column is bool
 };
 
 // ---------------------------------------------------------------- decode ----

@@ -62,6 +62,9 @@ struct packos_schema {
     std::vector<packos::DwDesc> fdw;   // lane-invariant descriptors (B % 4 == 0)
     int fix_T = 0, fix_lds = 0, fix_chunks = 0;
     int fix_maxseg = 0;                 // max column segments of any output dword (fdw)
+    std::vector<packos::DwDesc> ftdw, fxdw;  // k_encode_fixed_tile: single-source + X dwords
+    std::vector<uint32_t> fxq;
+    int fix_x_lds = 0, fix_tile_lds = 0;
 
     // decode program
     std::vector<packos::DecNode> dnodes;

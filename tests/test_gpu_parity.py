@@ -136,6 +136,28 @@ def test_random_fixed_schema_encode(seed):
     assert_same_encoding(chain, hc, 0, f"fixed seed {seed}")
 
 
+@pytest.mark.parametrize("variant", [13, 2, 1, 8])
+@pytest.mark.parametrize("seed", range(16))
+def test_fixed_kernel_variants(seed, variant):
+    """Every fixed-layout kernel on random fixed schemas padded (one extra
+    StringLen field) to a blob size the tile kernel takes (B % 4 == 0,
+    16 <= B <= 1024), with batch sizes that leave partial last tiles."""
+    chain = rand_chain(3000 + seed, allow_var=False, allow_null=False)
+    B = CompiledSchema(chain, 0).fixed_blob_size
+    pad = (-(B + 2)) % 4 + 4 * (seed % 4)
+    if pad == 0:
+        pad = 4
+    while B + 2 + pad < 16:
+        pad += 4
+    chain2 = SChain(*chain.Schemas, SStringLen(pad))
+    assert CompiledSchema(chain2, 0).fixed_blob_size % 4 == 0
+    n = [1, 63, 1000, 4097, 20001, 257][seed % 6]
+    hc = HostColumns.from_rows(chain2, rand_rows(chain2, n, seed, nil_p=0.0))
+    hc.valid = [None] * len(hc.valid)
+    assert_same_encoding(chain2, hc, 0, f"variant {variant} seed {seed} n {n}",
+                         flags=_lib.ENC_FIXED_VARIANT(variant))
+
+
 @pytest.mark.parametrize("n", [1, 2, 15, 16, 17, 63, 64, 65, 1000, 4097])
 def test_fixed_tail_tiles(n):
     cfg = CONFIGS["M"]

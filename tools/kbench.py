@@ -14,7 +14,7 @@ from packos_amd.api import CompiledSchema, DeviceColumns, EncodePlan  # noqa: E4
 from packos_amd.configs import CONFIGS, algorithmic_bytes, make_columns  # noqa: E402
 
 VARIANTS = {k: int(v) << 4 for k, v in (x.split("=") for x in os.environ.get(
-    "KBENCH_VARIANTS", "v1=1,v2=2,v4=4,v9=9,v10=10,v8=8").split(","))}
+    "KBENCH_VARIANTS", "v13=13,v2=2,v8=8").split(","))}
 TILES = [int(x) for x in os.environ.get("KBENCH_TILES", "16384").split(",")]
 
 

@@ -52,6 +52,26 @@ __global__ __launch_bounds__(256) void k_tile(const u32x4* __restrict__ in, u32x
     }
 }
 
+__global__ __launch_bounds__(256) void k_tilep(const u32x4* __restrict__ in, u32x4* __restrict__ out, size_t tin16,
+                                               size_t tout16, size_t ntiles) {
+    for (size_t b = blockIdx.x; b < ntiles; b += gridDim.x) {
+        const u32x4* src = in + b * tin16;
+        u32x4* dst = out + b * tout16;
+        u32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const size_t k = u * 256 + threadIdx.x;
+            v[u] = k < tin16 ? ld16<0>(src + k) : u32x4{0, 0, 0, 0};
+        }
+        unsigned x = v[0].x ^ v[1].y ^ v[2].z ^ v[3].w;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const size_t k = u * 256 + threadIdx.x;
+            if (k < tout16) st16<1>(dst + k, u32x4{x, (unsigned)k, v[u].z, v[u].w});
+        }
+    }
+}
+
 // same traffic, stores as dwords: wave instruction = 256 contiguous bytes
 // (the k_encode_fixed_dw store pattern); LDS round trip + barrier in between
 template <bool NT, bool VIA_LDS>
@@ -84,6 +104,40 @@ __global__ __launch_bounds__(256) void k_tile_dw(const u32x4* __restrict__ in, u
             unsigned x = v[u & 3].x ^ k;
             if (NT) __builtin_nontemporal_store(x, dst + k);
             else dst[k] = x;
+        }
+    }
+}
+
+// metric-M input shape: 8 SoA columns (widths 2,4,8,8,1,96,64,55); tile t
+// reads rows [64t, 64t+64) of every column as 16-B chunks (952 chunks) and
+// writes 16 KiB: the encode kernel's exact HBM traffic without its compute.
+// PERSIST: grid-stride over tiles (the persistent kernels' order).
+__constant__ unsigned c_w[8] = {2, 4, 8, 8, 1, 96, 64, 55};
+template <bool PERSIST>
+__global__ __launch_bounds__(256) void k_cols(const unsigned char* __restrict__ in, u32x4* __restrict__ out,
+                                              size_t ntiles, size_t nrows) {
+    for (size_t t = blockIdx.x; t < ntiles; t += PERSIST ? gridDim.x : ntiles) {
+        u32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            unsigned k = u * 256 + threadIdx.x, cb = 0;
+            size_t colbase = 0;
+            unsigned w = 0, cbk = 0;
+            size_t base = 0;
+            for (int g = 0; g < 8; g++) {
+                unsigned nch = 64 * c_w[g] / 16;
+                if (k >= cb) { w = c_w[g]; cbk = cb; base = colbase; }
+                cb += nch;
+                colbase += nrows * c_w[g];
+            }
+            v[u] = k < 952 ? *(const u32x4*)(in + base + t * 64 * w + (k - cbk) * 16) : u32x4{0, 0, 0, 0};
+        }
+        unsigned x = v[0].x ^ v[1].y ^ v[2].z ^ v[3].w;
+        u32x4* dst = out + t * 1024;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const unsigned k = u * 256 + threadIdx.x;
+            __builtin_nontemporal_store(u32x4{x, k, v[u].z, v[u].w}, (g4*)(dst + k));
         }
     }
 }
@@ -183,6 +237,11 @@ int main() {
     report("copy dword st nt", cb, timeit([&] { hipLaunchKernelGGL((k_tile_dw<true, false>), dim3(ntiles), dim3(256), 0, 0, a, (unsigned*)b, tin16, tout16); }, R));
     report("copy dword st plain", cb, timeit([&] { hipLaunchKernelGGL((k_tile_dw<false, false>), dim3(ntiles), dim3(256), 0, 0, a, (unsigned*)b, tin16, tout16); }, R));
     report("copy lds dword st nt", cb, timeit([&] { hipLaunchKernelGGL((k_tile_dw<true, true>), dim3(ntiles), dim3(256), 0, 0, a, (unsigned*)b, tin16, tout16); }, R));
+    report("cols 8 streams, tile per WG", cb, timeit([&] { hipLaunchKernelGGL((k_cols<false>), dim3(ntiles), dim3(256), 0, 0, (const unsigned char*)a, b, ntiles, ntiles * 64); }, R));
+    for (int g : {1024, 1280, 1536, 2048})
+        report(g == 1024 ? "cols persistent 1024" : g == 1280 ? "cols persistent 1280" : g == 1536 ? "cols persistent 1536" : "cols persistent 2048", cb,
+               timeit([&] { hipLaunchKernelGGL((k_cols<true>), dim3(g), dim3(256), 0, 0, (const unsigned char*)a, b, ntiles, ntiles * 64); }, R));
+    report("copy contiguous persistent 1280", cb, timeit([&] { hipLaunchKernelGGL((k_tilep), dim3(1280), dim3(256), 0, 0, a, b, tin16, tout16, ntiles); }, R));
 #define RW(SP, nm) \
     report(nm, (double)ntiles * tout, timeit([&] { hipLaunchKernelGGL((k_write<SP>), dim3(ntiles), dim3(256), 0, 0, b, tout16); }, R))
     RW(0, "write plain");
