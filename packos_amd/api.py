@@ -211,9 +211,10 @@ class EncodePlan:
     """Pre-bound encode of one batch into a preallocated arena: run() issues
     only C-ABI calls on `stream` (no host sync, no allocation) — what a serving
     loop or a graph capture replays.  Fixed-size batches: one encode call.
-    Variable-size batches: the size pass + scan, then the encode with
-    PACKOS_ENC_OFFSETS_READY; the arena is sized once at construction (one
-    host sync there) and `offsets` / `status` are refreshed by every run()."""
+    Variable-size batches: one packos_encode_batch call (sizes, look-back scan
+    and encode in a single kernel); the arena is sized once at construction
+    (one host sync there) and `offsets` / `status` are refreshed by every
+    run()."""
 
     def __init__(self, schema: CompiledSchema, cols: DeviceColumns, out=None, stream=None, flags: int = 0,
                  want_status: bool = False):
@@ -256,11 +257,11 @@ class EncodePlan:
             check(L.packos_encode_batch(self.schema.handle, self._arr, n, self.out.data_ptr(), self.out.numel(),
                                         None, stp, None, 0, self.flags, st), "packos_encode_batch")
             return self.out
-        check(L.packos_encoded_size_batch(self.schema.handle, self._arr, n, self.offsets.data_ptr(),
-                                          self.ws.data_ptr(), self.wsb, st), "packos_encoded_size_batch")
+        # one call: the single-pass kernel computes sizes, scans them (look-back)
+        # and encodes; `offsets` is rewritten by every run
         check(L.packos_encode_batch(self.schema.handle, self._arr, n, self.out.data_ptr(), self.out.numel(),
                                     self.offsets.data_ptr(), stp, self.ws.data_ptr(), self.wsb,
-                                    _lib.ENC_OFFSETS_READY | self.flags, st), "packos_encode_batch")
+                                    self.flags, st), "packos_encode_batch")
         return self.out
 
 

@@ -8,11 +8,14 @@
 //                   key bytes + funnel-shifted column bytes) and stores them
 //                   with global_store_dwordx4.  Pure byte/integer work, HBM
 //                   bound; no MFMA.
-//   k_encode_sizes  var-size schemas, pass 1: blob sizes (thread per blob)
-//   k_scan_*        exclusive scan of blob sizes -> out_offsets
-//   k_encode_var    var-size schemas, pass 2: one wavefront per blob; item
-//                   sizes -> wavefront prefix scan -> header words -> payload
-//                   staged in an LDS slot -> aligned 16-B stores
+//   k_stream_sizes  var-size schemas: blob sizes + decoupled look-back scan
+//                   -> out_offsets (encode_stream.inc)
+//   k_encode_stream var-size schemas: two bulk staging rounds into LDS, two
+//                   emitters per blob into an LDS image, 16-B stores
+//                   (encode_stream.inc)
+//   k_encode_var    per-blob fallback: one wavefront per blob; item sizes ->
+//                   wavefront prefix scan -> header words -> payload staged
+//                   in an LDS slot -> aligned 16-B stores
 //   k_decode        schema.DecodeBuffer semantics (SeqGetAccess + precheck),
 //                   one thread per blob, exact error/panic reporting
 //   k_get_field     GetAccess random-field gather
@@ -403,23 +406,7 @@ __device__ __forceinline__ uint32_t item_size(const EncItem& it, const EncCols& 
     return 0;
 }
 
-// pass 1: sizes[i] -> offs[i+1]; offs[0] = 0 (thread per blob)
-__global__ __launch_bounds__(kBlock) void k_encode_sizes(EncProgram P, EncCols cols, uint64_t* offs, uint64_t n) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) offs[0] = 0;
-    if (i >= n) return;
-    uint64_t pm = present_mask(P, cols, i);
-    uint32_t slack = 0;
-    uint64_t tot = 0;
-    for (int k = 0; k < P.n_items; k++) tot += item_size(P.items[k], cols, i, pm, &slack);
-    if (P.mode == PACKOS_MODE_PACKABLE) tot += slack;
-    offs[i + 1] = tot;
-}
-
-// ---- exclusive scan support (in place over offs[1..n]) -----------------
-constexpr int kScanPer = 4;
-constexpr int kScanTile = kBlock * kScanPer;
-
+// ---- scan support --------------------------------------------------------
 __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x, int lane) {
 #pragma unroll
     for (int d = 1; d < kWave; d <<= 1) {
@@ -427,66 +414,6 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x, int lane) {
         if (lane >= d) x += t;
     }
     return x;
-}
-
-// block-level inclusive scan of kScanTile elements; returns the tile total
-__device__ uint64_t block_scan_tile(uint64_t* v, uint64_t* s_w) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint64_t loc = 0;
-#pragma unroll
-    for (int k = 0; k < kScanPer; k++) { loc += v[k]; v[k] = loc; }
-    uint64_t incl = wave_incl_scan64(loc, lane);
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    uint64_t wave_off = 0, total = 0;
-    for (int w = 0; w < kWavesPerBlock; w++) {
-        if (w < wave) wave_off += s_w[w];
-        total += s_w[w];
-    }
-    uint64_t excl = wave_off + incl - loc;
-#pragma unroll
-    for (int k = 0; k < kScanPer; k++) v[k] += excl;
-    __syncthreads();
-    return total;
-}
-
-__global__ __launch_bounds__(kBlock) void k_scan_tiles(uint64_t* x, uint64_t n, uint64_t* sums) {
-    __shared__ uint64_t s_w[kWavesPerBlock];
-    uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
-    uint64_t v[kScanPer];
-#pragma unroll
-    for (int k = 0; k < kScanPer; k++) v[k] = base + k < n ? x[base + k] : 0;
-    uint64_t total = block_scan_tile(v, s_w);
-#pragma unroll
-    for (int k = 0; k < kScanPer; k++)
-        if (base + k < n) x[base + k] = v[k];
-    if (threadIdx.x == 0) sums[blockIdx.x] = total;
-}
-
-// exclusive scan of the tile sums, one workgroup, any count
-__global__ __launch_bounds__(kBlock) void k_scan_sums(uint64_t* sums, uint64_t nb) {
-    __shared__ uint64_t s_w[kWavesPerBlock];
-    uint64_t carry = 0;
-    for (uint64_t t0 = 0; t0 < nb; t0 += kScanTile) {
-        uint64_t base = t0 + (uint64_t)threadIdx.x * kScanPer;
-        uint64_t v[kScanPer], raw[kScanPer];
-#pragma unroll
-        for (int k = 0; k < kScanPer; k++) { raw[k] = v[k] = base + k < nb ? sums[base + k] : 0; }
-        uint64_t total = block_scan_tile(v, s_w);
-#pragma unroll
-        for (int k = 0; k < kScanPer; k++)
-            if (base + k < nb) sums[base + k] = carry + v[k] - raw[k];
-        carry += total;
-        __syncthreads();
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_scan_add(uint64_t* x, uint64_t n, const uint64_t* sums) {
-    uint64_t add = sums[blockIdx.x];
-    uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
-#pragma unroll
-    for (int k = 0; k < kScanPer; k++)
-        if (base + k < n) x[base + k] += add;
 }
 
 // One blob, one wavefront: item sizes -> wavefront prefix scan -> header
@@ -1319,6 +1246,8 @@ __global__ __launch_bounds__(kBlock) void k_var_copy(VarPlan V, const uint64_t* 
     }
 }
 
+#include "encode_stream.inc"
+
 // =========================================================================
 // decode: schema.DecodeBuffer, one thread per blob
 // =========================================================================
@@ -1945,7 +1874,8 @@ void packos_schema_free(packos_schema* s) {
 }
 
 // [scan tile sums][tile flags (k_var_copy)][value positions (u16, per var leaf x blob)]
-static size_t ws_scan_bytes(size_t n) { return (((n + kScanTile - 1) / kScanTile) + 16) * sizeof(uint64_t); }
+// (the scan tile sums also hold k_encode_stream's ticket + per-256-blob look-back words)
+static size_t ws_scan_bytes(size_t n) { return (((n + kS2T - 1) / kS2T) + 16) * sizeof(uint64_t); }
 static size_t ws_flag_bytes(size_t n) { return ((n + 63) / 64 + 4) * sizeof(uint32_t); }
 
 size_t packos_encode_workspace_size(const packos_schema* s, size_t n_blobs) {
@@ -1960,22 +1890,195 @@ size_t packos_encode_workspace_size(const packos_schema* s, size_t n_blobs) {
 static int size_pass(packos_schema* s, DeviceTables* t, const EncCols& ec, size_t n, uint64_t* offs, void* ws,
                      size_t ws_bytes, hipStream_t st) {
     if (!offs) { set_error("out_offsets required for a variable-size schema"); return PACKOS_E_INVALID; }
-    size_t nb = (n + kScanTile - 1) / kScanTile;
     if (!ws || ws_bytes < packos_encode_workspace_size(s, n)) {
         set_error("workspace too small");
         return PACKOS_E_WORKSPACE;
     }
-    const unsigned g = (unsigned)((n + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_encode_sizes, dim3(std::max(1u, g)), dim3(kBlock), 0, st, t->enc, ec, offs, (uint64_t)n);
-    if (n) {
-        uint64_t* sums = (uint64_t*)ws;
-        hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)nb), dim3(kBlock), 0, st, offs + 1, (uint64_t)n, sums);
-        hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(kBlock), 0, st, sums, (uint64_t)nb);
-        hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(kBlock), 0, st, offs + 1, (uint64_t)n,
-                           (const uint64_t*)sums);
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(offs, 0, sizeof(uint64_t), st));
+        return PACKOS_OK;
     }
+    // k_stream_sizes: ticket + per-tile look-back words at the start of ws
+    const uint64_t ntiles = (n + kSzTile - 1) / kSzTile;
+    HIP_TRY(hipMemsetAsync(ws, 0, (ntiles + 1) * sizeof(uint64_t), st));
+    static unsigned long long* zprof = nullptr;  // debug: PACKOS_STREAM_PROF=1 prints phase clocks
+    const bool want_prof = getenv("PACKOS_STREAM_PROF") != nullptr;
+    if (want_prof && !zprof) HIP_TRY(hipMalloc(&zprof, 16 * sizeof(unsigned long long)));
+    if (want_prof) HIP_TRY(hipMemsetAsync(zprof, 0, 16 * sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_stream_sizes, dim3((unsigned)ntiles), dim3(kBlock),
+                       sizes_lds_bytes((int)s->items.size(), (int)s->conts.size()), st, t->enc, ec, (uint64_t*)ws,
+                       offs, (uint64_t)n, want_prof ? zprof : nullptr);
     HIP_TRY(hipGetLastError());
+    if (want_prof) {
+        unsigned long long h[16];
+        HIP_TRY(hipMemcpyAsync(h, zprof, sizeof(h), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        fprintf(stderr, "sizes tiles=%llu clocks/tile:", (unsigned long long)ntiles);
+        for (int i = 0; i < 5; i++) fprintf(stderr, " p%d=%.0f", i, (double)h[8 + i] / ntiles);
+        fprintf(stderr, "\n");
+    }
     return PACKOS_OK;
+}
+
+// k_encode_stream plan for one call (kernel argument).  false: the schema /
+// columns exceed the plan's tables or LDS, use the tiled encoder.
+static bool stream_plan(const packos_schema* s, const EncCols& ec, S2Plan& S) {
+    memset(&S, 0, sizeof(S));
+    const uint32_t NI = (uint32_t)s->items.size();
+    if (NI > (uint32_t)kS2Items || s->conts.size() > (size_t)kS2Conts) return false;
+    // value staging (fix_cap / var_cap) is off by default: measured on the box, the LDS it
+    // takes costs more occupancy than the HBM latency it hides (C3 0.162 -> 0.132 ms)
+    uint32_t longv = 48, img_cap = 14336, fix_cap = 0, var_cap = 0, var_per = 36;
+    if (const char* e = getenv("PACKOS_STREAM_LONG")) longv = (uint32_t)std::max(32, std::min(4096, atoi(e)));
+    if (const char* e = getenv("PACKOS_STREAM_IMG")) img_cap = (uint32_t)std::max(2048, std::min(49152, atoi(e)));
+    if (const char* e = getenv("PACKOS_STREAM_VAR")) var_cap = (uint32_t)std::max(0, std::min(32768, atoi(e)));
+    if (const char* e = getenv("PACKOS_STREAM_FIX")) fix_cap = (uint32_t)std::max(0, std::min(49152, atoi(e)));
+    if (const char* e = getenv("PACKOS_STREAM_VPER")) var_per = (uint32_t)std::max(4, std::min(256, atoi(e)));
+    auto al16 = [](uint32_t x) { return (x + 15u) & ~15u; };
+    uint32_t o = 0, cb = 0;
+    std::vector<int> val_seg(kMaxCols, -1), fix_seg(kMaxCols, -1), off_seg(kMaxCols, -1), var_slot(kMaxCols, -1);
+    auto add_seg = [&](const uint8_t* src, uint32_t w, bool extra) -> int {
+        if (S.nseg >= kS2Seg) return -1;
+        const int k = S.nseg++;
+        const uint32_t bytes = (uint32_t)(kS2T + (extra ? 1 : 0)) * w;
+        const uint32_t maxch = (bytes + 15) / 16 + 1;
+        S.seg_src[k] = src;
+        S.seg_w[k] = w;
+        S.seg_lds[k] = o;
+        S.seg_cb[k] = cb;
+        if (extra) S.seg_extra |= 1u << k;
+        cb += maxch;
+        o += maxch * 16 + 16;   // +16: padding for 2-dword unaligned reads
+        return k;
+    };
+    // validity columns, var offsets, fixed columns (up to fix_cap bytes per tile)
+    for (size_t c = 0; c < s->col_node.size() && c < (size_t)kMaxCols; c++) {
+        if (!ec.valid[c]) continue;
+        if ((val_seg[c] = add_seg(ec.valid[c], 1, false)) < 0) return false;
+    }
+    uint32_t fix_bytes = 0, worst = 0;
+    for (const EncItem& it : s->items) {
+        if (it.type == IT_VAR) {
+            if (off_seg[it.col] < 0 && (off_seg[it.col] = add_seg((const uint8_t*)ec.off[it.col], 4, true)) < 0)
+                return false;
+            worst += longv;
+            continue;
+        }
+        worst += it.type == IT_HDR ? it.size : std::min(it.size, longv);
+        if (it.type != IT_FIXED || fix_seg[it.col] >= 0) continue;
+        if (fix_bytes + kS2T * it.size <= fix_cap && S.nseg < kS2Seg) {
+            fix_seg[it.col] = add_seg(ec.data[it.col], it.size, false);
+            fix_bytes += kS2T * it.size;
+        }
+    }
+    S.seg_cb[S.nseg] = cb;
+    // var columns staged in the same load round (their tile range known from
+    // two uniform offset loads)
+    uint32_t vb = 0;
+    for (const EncItem& it : s->items) {
+        if (it.type != IT_VAR || var_slot[it.col] >= 0 || S.nvar >= kS2Var) continue;
+        const uint32_t bud = std::min<uint32_t>(al16(kS2T * var_per + 32), var_cap > vb ? var_cap - vb : 0);
+        if (bud < 512) break;
+        const int k = S.nvar++;
+        var_slot[it.col] = k;
+        S.var_off[k] = ec.off[it.col];
+        S.var_data[k] = ec.data[it.col];
+        S.var_lds[k] = o;
+        S.var_bud[k] = bud;
+        S.var_cb[k] = vb / 16;
+        vb += bud;
+        o += bud + 16;
+    }
+    S.var_cb[S.nvar] = vb / 16;
+    // per-item plan
+    uint32_t nlong = 0;
+    for (uint32_t k = 0; k < NI; k++) {
+        const EncItem& it = s->items[k];
+        S2K& x = S.item[k];
+        x.type = it.type;
+        x.size = (uint16_t)std::min<uint32_t>(it.size, 0xFFFFu);
+        x.cont = (uint16_t)it.cont;
+        x.col = it.col;
+        x.flags = it.is_bool ? SD_BOOL : 0;
+        if (it.type == IT_HDR) {
+            x.la = (uint16_t)(s->ihr[k] & 0xFFFFu);
+            x.lv = (uint16_t)(s->ihr[k] >> 16);
+        } else if (it.type == IT_CONST) {
+            if (it.lit > 0xFFFFu) return false;
+            x.la = (uint16_t)it.lit;
+            if (it.size > longv) { x.flags |= SD_LONG; nlong++; }
+        } else if (it.type == IT_FIXED) {
+            const int sg = fix_seg[it.col];
+            if (sg >= 0) {
+                x.la = (uint16_t)S.seg_lds[sg];
+                x.src15 = (uint8_t)((uintptr_t)ec.data[it.col] & 15);
+                x.flags |= SD_STAGED;
+                if (it.size == 1 || it.size == 2 || it.size == 4 || it.size == 8) x.flags |= SD_DIRECT;
+            }
+            else if ((it.size == 1 || it.size == 2 || it.size == 4 || it.size == 8) &&
+                     ((uintptr_t)ec.data[it.col] % it.size) == 0)
+                x.flags |= SD_GDIRECT;
+            if (!(x.flags & (SD_DIRECT | SD_GDIRECT)) && it.size > longv) { x.flags |= SD_LONG; nlong++; }
+            if (it.nullable && val_seg[it.col] >= 0) {
+                x.flags |= SD_VALID;
+                x.lv = (uint16_t)S.seg_lds[val_seg[it.col]];
+                x.vsrc15 = (uint8_t)((uintptr_t)ec.valid[it.col] & 15);
+            }
+        } else {
+            const int sg = off_seg[it.col];
+            x.la = (uint16_t)S.seg_lds[sg];
+            x.src15 = (uint8_t)((uintptr_t)ec.off[it.col] & 15);
+            x.flags |= SD_LONG;
+            nlong++;
+            if (var_slot[it.col] >= 0) { x.flags |= SD_VSLOT; x.lv = (uint16_t)var_slot[it.col]; }
+        }
+    }
+    for (size_t c = 0; c < s->conts.size(); c++) {
+        const EncCont& ct = s->conts[c];
+        S2KCont& x = S.cont[c];
+        x.parent = ct.parent;
+        x.lv = 0xFFFFu;
+        if (ct.valid_col >= 0 && val_seg[ct.valid_col] >= 0) {
+            x.lv = (uint16_t)S.seg_lds[val_seg[ct.valid_col]];
+            x.vsrc15 = (uint8_t)((uintptr_t)ec.valid[ct.valid_col] & 15);
+        }
+    }
+    S.pos_lds = o;
+    o += al16(2u * kS2T * (NI + 1));
+    uint32_t img = (uint32_t)std::min<uint64_t>(img_cap, (uint64_t)kS2T * worst + 32);
+    img = std::max<uint32_t>(img, std::max<uint32_t>(2048u, 16u * (NI + 1) * kWavesPerBlock));
+    S.img_bytes = al16(img);
+    S.img_lds = o;
+    o += S.img_bytes + 16;
+    S.hole_cap = std::min<uint32_t>(nlong * kS2T, 1024u);
+    S.hole_lds = o;
+    o += al16(4 * S.hole_cap + 4 * (S.hole_cap + 2) + 8 * S.hole_cap);
+    S.blob_lds = o;
+    o += al16((uint32_t)sizeof(S2Blob) * kS2T);
+    S.desc_lds = o;
+    o += (uint32_t)sizeof(S2Desc) * NI;
+    S.hdr_lds = o;
+    o += al16((uint32_t)sizeof(S2Hdr) * (uint32_t)s->hdrs.size());
+    S.hw_lds = o;
+    o += al16(2u * kS2T * (uint32_t)s->hdrs.size()) + 16;
+    S.grp_lds = o;
+    o += S.hole_cap ? 2u * kS2Grp : 0u;
+    S.misc_lds = o;
+    o += 64;
+    S.lds_total = o;
+    S.longv = longv;
+    // emitter split: the item boundary closest to half the estimated blob bytes
+    uint64_t tot = 0;
+    for (const EncItem& it : s->items) tot += it.type == IT_VAR ? 32u : it.size;
+    uint64_t run = 0, best = ~0ull;
+    S.mid = NI;
+    for (uint32_t k = 0; k <= NI; k++) {
+        const uint64_t d = 2 * run > tot ? 2 * run - tot : tot - 2 * run;
+        if (d < best) { best = d; S.mid = k; }
+        if (k < NI) run += s->items[k].type == IT_VAR ? 32u : s->items[k].size;
+    }
+    if (const char* e = getenv("PACKOS_STREAM_MID")) S.mid = (uint32_t)std::max(0, std::min((int)NI, atoi(e)));
+    return o <= 64 * 1024;
 }
 
 int packos_encoded_size_batch(const packos_schema* cs, const packos_column* cols, size_t n, uint64_t* out_offsets,
@@ -2087,11 +2190,44 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
         HIP_TRY(hipGetLastError());
         return PACKOS_OK;
     }
-    if (!(flags & PACKOS_ENC_OFFSETS_READY)) {
-        if ((r = size_pass(s, t, ec, n, out_offsets, ws, ws_bytes, st))) return r;
-    } else if (!out_offsets) {
-        set_error("PACKOS_ENC_OFFSETS_READY without out_offsets");
+    const bool offs_ready = (flags & PACKOS_ENC_OFFSETS_READY) != 0;
+    if (!out_offsets) {
+        set_error(offs_ready ? "PACKOS_ENC_OFFSETS_READY without out_offsets"
+                             : "out_offsets required for a variable-size schema");
         return PACKOS_E_INVALID;
+    }
+    // default: k_stream_sizes (look-back scan; skipped when the caller's offsets
+    // are ready) + k_encode_stream.  PACKOS_VAR_KERNEL=tile selects the
+    // two-kernel tiled encoder below.
+    const char* vk = getenv("PACKOS_VAR_KERNEL");
+    const bool want_stream = !(flags & PACKOS_ENC_FORCE_GENERIC) && !(vk && strcmp(vk, "tile") == 0);
+    S2Plan SP;
+    if (want_stream && s->conts.size() <= 64 && stream_plan(s, ec, SP)) {
+        if (!offs_ready) {
+            if ((r = size_pass(s, t, ec, n, out_offsets, ws, ws_bytes, st))) return r;
+        }
+        const uint64_t ntiles = (n + kS2T - 1) / kS2T;
+        static unsigned long long* sprof = nullptr;  // debug: PACKOS_STREAM_PROF=1 prints phase clocks
+        const bool want_prof = getenv("PACKOS_STREAM_PROF") != nullptr;
+        if (want_prof && !sprof) HIP_TRY(hipMalloc(&sprof, 16 * sizeof(unsigned long long)));
+        if (want_prof) HIP_TRY(hipMemsetAsync(sprof, 0, 16 * sizeof(unsigned long long), st));
+        SP.prof = want_prof ? sprof : nullptr;
+        hipLaunchKernelGGL(k_encode_stream, dim3((unsigned)ntiles), dim3(kBlock), SP.lds_total, st, t->enc, ec, SP,
+                           (const uint64_t*)out_offsets, out, cap, (uint64_t)n, status);
+        HIP_TRY(hipGetLastError());
+        if (want_prof) {
+            unsigned long long h[16];
+            HIP_TRY(hipMemcpyAsync(h, sprof, sizeof(h), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            fprintf(stderr, "stream lds=%u img=%u holes=%u segs=%d vars=%d mid=%u tiles=%llu clocks/tile:",
+                    SP.lds_total, SP.img_bytes, SP.hole_cap, SP.nseg, SP.nvar, SP.mid, (unsigned long long)ntiles);
+            for (int i = 0; i < 8; i++) fprintf(stderr, " p%d=%.0f", i, (double)h[i] / ntiles);
+            fprintf(stderr, "\n");
+        }
+        return PACKOS_OK;
+    }
+    if (!offs_ready) {
+        if ((r = size_pass(s, t, ec, n, out_offsets, ws, ws_bytes, st))) return r;
     }
     const size_t npos = s->items.size() + 1;
     int vt = 128;

@@ -25,11 +25,24 @@ def torch():
     return t
 
 
-def gpu_encode(chain, hc, mode=0, flags=0):
+def gpu_encode(chain, hc, mode=0, flags=0, fused=False):
+    """fused=True: size the arena with the size pass, then encode WITHOUT
+    PACKOS_ENC_OFFSETS_READY into poisoned offsets, so the single-pass kernel's
+    own sizes + look-back scan must produce them."""
     T = torch()
     s = CompiledSchema(chain, mode)
     dc = DeviceColumns.from_host(s, hc, "cuda:0")
     r = encode_batch(s, dc, flags=flags)
+    if fused and r.blob_size < 0 and hc.n:
+        L = _lib.lib()
+        n = hc.n
+        wsb = L.packos_encode_workspace_size(s.handle, n)
+        ws = T.full((wsb,), 0xAB, dtype=T.uint8, device="cuda:0")
+        r.offsets.fill_(-1)
+        r.arena.fill_(0xCD)
+        assert L.packos_encode_batch(s.handle, dc.ctypes_array(), n, r.arena.data_ptr(), r.arena.numel(),
+                                     r.offsets.data_ptr(), r.status.data_ptr(), ws.data_ptr(), wsb, flags,
+                                     None) == 0, L.packos_last_error().decode()
     T.cuda.synchronize()
     arena = r.arena[: r.total].cpu().numpy()
     offs = r.offsets.cpu().numpy().astype(np.uint64)
@@ -37,9 +50,9 @@ def gpu_encode(chain, hc, mode=0, flags=0):
     return arena, offs, st
 
 
-def assert_same_encoding(chain, hc, mode, what="", flags=0):
+def assert_same_encoding(chain, hc, mode, what="", flags=0, fused=False):
     a0, o0, s0 = ob.encode(chain, hc, mode, nthreads=8)
-    a1, o1, s1 = gpu_encode(chain, hc, mode, flags)
+    a1, o1, s1 = gpu_encode(chain, hc, mode, flags, fused)
     assert np.array_equal(o0, o1), f"{what}: offsets differ"
     if not np.array_equal(a0, a1):
         bad = int(np.nonzero(a0 != a1)[0][0])
@@ -69,12 +82,67 @@ def test_golden_cross_api(case):
 
 
 # --------------------------------------------------------------- encode ----
+STREAM_KNOBS = [{}, {"PACKOS_STREAM_IMG": "4096"}, {"PACKOS_STREAM_LONG": "32"}, {"PACKOS_STREAM_LONG": "200"},
+                {"PACKOS_STREAM_IMG": "6000", "PACKOS_STREAM_LONG": "32"}, {"PACKOS_STREAM_VAR": "0"},
+                {"PACKOS_STREAM_FIX": "0"}, {"PACKOS_STREAM_MID": "0"}, {"PACKOS_STREAM_MID": "1"},
+                {"PACKOS_STREAM_MID": "99"}, {"PACKOS_STREAM_VAR": "600", "PACKOS_STREAM_FIX": "300"}]
+
+
+@pytest.mark.parametrize("fused", [False, True], ids=["offsets_ready", "single_pass"])
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("seed", range(60))
-def test_random_schema_encode(seed, mode):
+def test_random_schema_encode(seed, mode, fused):
+    # default var path: k_encode_stream (caller offsets, or its own look-back scan)
+    chain = rand_chain(seed)
+    hc = HostColumns.from_rows(chain, rand_rows(chain, 257 + 300 * (seed % 3), seed * 7 + 1))
+    assert_same_encoding(chain, hc, mode, f"seed {seed}", fused=fused)
+
+
+@pytest.mark.parametrize("knobs", STREAM_KNOBS[1:], ids=lambda k: ",".join(f"{a[14:]}={b}" for a, b in k.items()))
+@pytest.mark.parametrize("seed", range(0, 60, 6))
+def test_random_schema_encode_stream_knobs(seed, knobs, monkeypatch):
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    chain = rand_chain(seed)
+    hc = HostColumns.from_rows(chain, rand_rows(chain, 700, seed * 7 + 3))
+    assert_same_encoding(chain, hc, seed % 2, f"knobs {knobs} seed {seed}", fused=True)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("seed", range(20))
+def test_random_schema_encode_tile_kernel(seed, mode, monkeypatch):
+    # PACKOS_VAR_KERNEL=tile: the two-kernel tiled encoder (size pass + tile kernel)
+    monkeypatch.setenv("PACKOS_VAR_KERNEL", "tile")
     chain = rand_chain(seed)
     hc = HostColumns.from_rows(chain, rand_rows(chain, 257, seed * 7 + 1))
-    assert_same_encoding(chain, hc, mode, f"seed {seed}")
+    assert_same_encoding(chain, hc, mode, f"tile seed {seed}")
+
+
+@pytest.mark.parametrize("fused", [False, True], ids=["offsets_ready", "single_pass"])
+@pytest.mark.parametrize("knobs", STREAM_KNOBS, ids=lambda k: ",".join(f"{a[14:]}={b}" for a, b in k.items()) or "default")
+def test_stream_long_values_and_budgets(knobs, fused, monkeypatch):
+    """k_encode_stream: values around the long-value threshold at every 16-B
+    alignment (head / hole / tail split), adjacent long values, nil
+    containers; small image budgets that push tiles onto the per-blob
+    fallback, unstaged var / fixed columns (HBM reads), every emitter split."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    img = knobs.get("PACKOS_STREAM_IMG")
+    longv = knobs.get("PACKOS_STREAM_LONG")
+    chain = SChain(SInt16, SVariableString(), SVariableString(), STuple(SVariableString(), SInt16),
+                   SStringLen(100))
+    rng = np.random.default_rng(11)
+    rows = []
+    lens = [0, 1, 15, 16, 17, 31, 32, 33, 48, 63, 64, 65, 66, 79, 80, 81, 95, 96, 97, 127, 128, 129, 200, 513]
+    for i in range(1100):
+        a = lens[int(rng.integers(0, len(lens)))] + (i % 3)
+        b = lens[int(rng.integers(0, len(lens)))]
+        c = int(rng.integers(0, 300)) if i % 7 else 4000
+        rows.append([i, "a" * a, bytes(rng.integers(32, 127, b, dtype=np.uint8)).decode(),
+                     None if rng.random() < 0.15 else ["t" * c, -i], "p" * 100])
+    hc = HostColumns.from_rows(chain, rows)
+    for mode in (0, 1):
+        assert_same_encoding(chain, hc, mode, f"stream img={img} longv={longv} mode={mode}", fused=fused)
 
 
 @pytest.mark.parametrize("mode", [0, 1])
@@ -87,8 +155,9 @@ def test_random_schema_encode_wave_kernel(seed, mode):
     assert_same_encoding(chain, hc, mode, f"wave seed {seed}", flags=_lib.ENC_FORCE_GENERIC)
 
 
+@pytest.mark.parametrize("kernel", ["stream", "stream_fused", "tile"])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_var_tile_runs_and_fallbacks(mode):
+def test_var_tile_runs_and_fallbacks(mode, kernel, monkeypatch):
     """Tiled var encode: runs split at 8 KiB windows, runs larger than the LDS
     budget, blobs > 64 KiB (whole-tile fallback), and ragged last tiles."""
     chain = SChain(SInt16, SVariableString(), STuple(SVariableString(), SInt16))
@@ -99,7 +168,9 @@ def test_var_tile_runs_and_fallbacks(mode):
         ln = int(rng.integers(0, 40)) if r < 0.7 else int(rng.integers(3000, 12000)) if r < 0.97 else 70_000
         rows.append([i, "s" * ln, None if rng.random() < 0.1 else ["t" * int(rng.integers(0, 300)), -i]])
     hc = HostColumns.from_rows(chain, rows)
-    assert_same_encoding(chain, hc, mode, "tile edges")
+    if kernel == "tile":
+        monkeypatch.setenv("PACKOS_VAR_KERNEL", "tile")
+    assert_same_encoding(chain, hc, mode, f"tile edges {kernel}", fused=kernel == "stream_fused")
 
 
 def test_var_encode_capacity_overrun():
@@ -168,7 +239,9 @@ def test_fixed_tail_tiles(n):
                                     ("C4", 65_537), ("C5", 20_000)])
 def test_configs_vs_oracle(name, n):
     cfg = CONFIGS[name]
-    assert_same_encoding(cfg.chain, make_columns(cfg, n=n), cfg.mode, name)
+    hc = make_columns(cfg, n=n)
+    assert_same_encoding(cfg.chain, hc, cfg.mode, name)
+    assert_same_encoding(cfg.chain, hc, cfg.mode, name + " single pass", fused=True)
 
 
 def test_overflow_13bit_and_large_blob():

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-config GPU vs CPU rates: for every BASELINE config,
-device-resident encode (EncodePlan replay: for var schemas size pass + scan +
-encode) and decode (DecodeBuffer semantics) on cuda:0, the CPU oracle
+device-resident encode (EncodePlan replay: for var schemas one single-pass
+encode call) and decode (DecodeBuffer semantics) on cuda:0, the CPU oracle
 (C restatement of the reference, 'port') on the host cores over a bounded
 sample, the speed-ups, and for var configs a chunked pinned
 H2D + encode + D2H rate.  One JSON line per config.
@@ -74,8 +74,8 @@ def cpu_rates(cfg, n, seconds):
 
 
 def e2e_var(schema, hc, plan_total, reps=1):
-    """Chunked pinned H2D (columns) + size pass + encode + D2H (arena), two
-    streams double-buffered.  Sizes per chunk come from the device size pass;
+    """Chunked pinned H2D (columns) + single-pass encode + D2H (arena), two
+    streams double-buffered.  Offsets per chunk come from the encode kernel;
     the D2H byte count from the host-side layout (flat chains: base + var)."""
     from packos_amd import _lib
     L = _lib.lib()
@@ -150,16 +150,15 @@ def e2e_var(schema, hc, plan_total, reps=1):
                 dc = DeviceColumns(schema, m, cols, offs_d, [None] * len(cols))
                 arr = dc.ctypes_array()
                 sp_ = st.cuda_stream
-                L.packos_encoded_size_batch(schema.handle, arr, m, od.data_ptr(), ws.data_ptr(), wsb, sp_)
                 L.packos_encode_batch(schema.handle, arr, m, outd.data_ptr(), outd.numel(), od.data_ptr(), None,
-                                      ws.data_ptr(), wsb, _lib.ENC_OFFSETS_READY, sp_)
+                                      ws.data_ptr(), wsb, 0, sp_)
                 nb = int(boff[s0 + m] - boff[s0])
                 out_host[int(boff[s0]):int(boff[s0]) + nb].copy_(outd[:nb], non_blocking=True)
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / reps
     ok = bool(int(boff[-1]) == plan_total)
     return {"million_blobs_per_s": round(n / el / 1e6, 3), "gib_per_s_out": round(int(boff[-1]) / el / 2 ** 30, 3),
-            "chunks": nch, "size_check": ok, "note": "pinned H2D + size pass + encode + D2H, 2 streams"}, out_host
+            "chunks": nch, "size_check": ok, "note": "pinned H2D + single-pass encode + D2H, 2 streams"}, out_host
 
 
 def main():
@@ -197,7 +196,7 @@ def main():
                 "encode": {"ms": round(enc_ms, 4), "million_blobs_per_s": round(g_enc, 2),
                            "GBps_algorithmic": round(alg_enc / enc_ms / 1e6, 1),
                            "roofline_frac": round(alg_enc / enc_ms / 1e6 / 8000.0, 4),
-                           "includes": "encode" if fixed else "size pass + scan + encode"},
+                           "includes": "encode" if fixed else "single-pass encode (sizes + look-back scan + encode)"},
                 "decode": {"ms": round(dec_ms, 4), "million_blobs_per_s": round(g_dec, 2),
                            "GBps_algorithmic": round(alg_dec / dec_ms / 1e6, 1),
                            "fast_path": s.decode_fast, "nonzero_status": bad},
