@@ -1537,94 +1537,123 @@ __global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecPro
     uint32_t* fail = chk + 2 * QW;
     LDec* ltab = (LDec*)(fail + ((T + 1) & ~1u));
 
-    uint64_t base = blob0 * B;
+    // the tile base is one scalar load; whether the tile's blobs really lie
+    // back to back at stride B is checked while the staging DMA is in flight
+    typedef __attribute__((address_space(4))) const uint64_t c_u64;
+    const uint64_t base = offs ? ((c_u64*)(uintptr_t)offs)[blob0] : blob0 * B;
+    const bool aligned_base = (base & 15) == 0;
     bool ok = true;
-    if (offs) {
-        base = offs[blob0];
-        for (uint32_t j = tid; j <= rows; j += kBlock) ok &= offs[blob0 + j] == base + (uint64_t)j * B;
-        ok &= (base & 15) == 0;
-    }
     for (uint32_t q = tid; q < 2 * QW; q += kBlock) chk[q] = F.chk[q];
     for (uint32_t j = tid; j < rows; j += kBlock) fail[j] = 0;
-    for (int c = tid; c < F.n_cols; c += kBlock) {
-        const DecFix fc = F.cols[c];
-        ltab[c] = LDec{cols.data[fc.col], fc.width, fc.blob_off, fc.flags, fc.magic, fc.unit_begin, 0};
+    if (tid < kWave)   // uniform item walk: EncCols/DecCols are kernel arguments (no lane-indexed reads)
+        for (int c = 0; c < F.n_cols; c++) {
+            const DecFix fc = F.cols[c];
+            const LDec x{cols.data[fc.col], fc.width, fc.blob_off, fc.flags, fc.magic, fc.unit_begin, 0};
+            if (tid == 0) ltab[c] = x;
+        }
+    // 1. stage: global -> LDS with global_load_lds_dwordx4 (every chunk of the
+    //    tile in flight at once; a load -> ds_write loop waits per chunk)
+    const uint32_t bytes = rows * B;
+    if (aligned_base) {
+        const uint8_t* src = arena + base;
+        const uint32_t n16 = bytes >> 4, lane = tid & 63, c00 = tid & ~63u;
+        const uint32_t lds0 = (uint32_t)(uintptr_t)lds_raw;
+        for (uint32_t c0 = c00; c0 < n16; c0 += kBlock)
+            if (c0 + lane < n16) dma16(src + 16u * (c0 + lane), __builtin_amdgcn_readfirstlane(lds0 + 16u * c0));
+        for (uint32_t k = n16 * 16 + tid; k < bytes; k += kBlock) lds_raw[k] = src[k];
     }
+    if (offs) {
+        for (uint32_t j = tid; j <= rows; j += kBlock) ok &= offs[blob0 + j] == base + (uint64_t)j * B;
+        ok &= aligned_base;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!__syncthreads_and(ok)) {
         for (uint32_t j = tid; j < rows; j += kBlock) {
             const uint64_t i = blob0 + j;
-            status[i] = decode_blob(P, cols, GReader{arena}, offs[i], offs[i + 1], i);
+            status[i] = decode_blob(P, cols, GReader{arena}, offs ? offs[i] : i * B, offs ? offs[i + 1] : (i + 1) * B, i);
         }
         return;
     }
-    // 1. stage
-    const uint32_t bytes = rows * B;
-    {
-        const g_u32x4* src = (const g_u32x4*)(arena + base);
-        const uint32_t n16 = bytes >> 4;
-        for (uint32_t k = tid; k < n16; k += kBlock) ((u32x4*)lds)[k] = __builtin_nontemporal_load(src + k);
-        const uint8_t* src1 = arena + base;
-        for (uint32_t k = n16 * 16 + tid; k < bytes; k += kBlock) lds_raw[k] = src1[k];
+    // 2. constant-byte check, over the blob dwords that HOLD constant bytes
+    //    (header words, literals: 5 of 64 for metric M), compacted by ballot
+    uint32_t* cq = fail + ((T + 1) & ~1u) + ((sizeof(LDec) * F.n_cols + 3) >> 2);  // after ltab
+    if (tid < kWave) {
+        uint32_t nq = 0;
+        for (uint32_t q0 = 0; q0 < QW; q0 += kWave) {
+            const uint32_t q = q0 + tid;
+            const bool has = q < QW && chk[2 * q] != 0u;
+            const uint64_t m = __ballot(has);
+            if (has) cq[1 + nq + __popcll(m & ((1ull << tid) - 1))] = q;
+            nq += __popcll(m);
+        }
+        if (tid == 0) cq[0] = nq;
     }
     __syncthreads();
-    // 2. constant-byte check
-    if ((B & 3) == 0) {
-        const uint32_t Q = B >> 2;
-        for (uint32_t e = tid; e < bytes / 4; e += kBlock) {
-            const uint32_t j = F.q_magic ? __umulhi(e, F.q_magic) : e;
-            const uint32_t q = e - j * Q;
-            if ((lds[e] & chk[2 * q]) != chk[2 * q + 1]) fail[j] = 1;
-        }
-    } else {
-        for (uint32_t t = tid; t < bytes; t += kBlock) {
-            const uint32_t j = __umulhi(t, F.b_magic);
-            const uint32_t p = t - j * B, sh = 8 * (p & 3);
-            const uint32_t m = (chk[2 * (p >> 2)] >> sh) & 0xFFu, v = (chk[2 * (p >> 2) + 1] >> sh) & 0xFFu;
-            if ((lds_u8(lds, t) & m) != v) fail[j] = 1;
+    {
+        const uint32_t nq = cq[0];
+        const uint32_t nq_magic = nq > 1 ? (uint32_t)((0x100000000ull + nq - 1) / nq) : 0u;
+        for (uint32_t e = tid; e < rows * nq; e += kBlock) {
+            const uint32_t j = nq > 1 ? __umulhi(e, nq_magic) : e;
+            const uint32_t q = cq[1 + e - j * nq];
+            const uint32_t a = j * B + 4 * q;   // blob dword q (B % 4 == 0: aligned)
+            const uint32_t v = (B & 3) == 0 ? lds[a >> 2] : lds_bytes4(lds, a);
+            if ((v & chk[2 * q]) != chk[2 * q + 1]) fail[j] = 1;
         }
     }
-    // 3. columns: unit u = 16 output bytes of one column
-    for (uint32_t u = tid; u < (uint32_t)F.total_units; u += kBlock) {
-        int sel = 0;
-        for (int c = 1; c < F.n_cols; c++) sel = u >= ltab[c].unit_begin ? c : sel;
-        const LDec L = ltab[sel];
-        const uint32_t w = L.width;
-        const uint32_t t0 = (u - L.unit_begin) * 16;
-        const uint32_t R = rows * w;
-        if (t0 >= R) continue;
-        uint8_t* dst = L.dst + blob0 * w + t0;
-        if (t0 + 16 <= R) {
-            u32x4 v;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t b = t0 + 4 * k;
-                uint32_t j = w > 1 ? __umulhi(b, L.magic) : b;
-                uint32_t r = b - j * w;
+    // 3. columns: uniform walk over the columns; threads stride the column's
+    //    output dwords (consecutive lanes -> consecutive dwords: 256-B stores)
+    for (int c = 0; c < F.n_cols; c++) {
+        const LDec L = ltab[c];
+        const uint32_t w = L.width, R = rows * w, D = R >> 2;
+        uint32_t* dst = (uint32_t*)(L.dst + blob0 * w);   // 4-B aligned: T*w % 4 == 0, base 16-B aligned
+        if ((w & 3) == 0) {
+            for (uint32_t d = tid; d < D; d += kBlock) {
+                const uint32_t b = 4 * d;
+                const uint32_t j = __umulhi(b, L.magic);
+                const uint32_t a = j * B + L.blob_off + (b - j * w);
+                __builtin_nontemporal_store(lds_bytes4(lds, a), dst + d);
+            }
+        } else if (w == 2) {   // a dword = rows 2d, 2d+1
+            for (uint32_t d = tid; d < D; d += kBlock) {
+                const uint32_t a = 2 * d * B + L.blob_off;
+                const uint32_t x = (lds_bytes4(lds, a) & 0xFFFFu) | (lds_bytes4(lds, a + B) << 16);
+                __builtin_nontemporal_store(x, dst + d);
+            }
+        } else if (w > 4 && !(L.flags & 1u)) {   // most dwords sit inside one row
+            for (uint32_t d = tid; d < D; d += kBlock) {
+                const uint32_t b = 4 * d;
+                const uint32_t j = __umulhi(b, L.magic);
+                const uint32_t r = b - j * w;
                 uint32_t x;
                 if (r + 4 <= w) {
-                    const uint32_t a = j * B + L.blob_off + r;
-                    x = __builtin_amdgcn_alignbyte(lds[(a >> 2) + 1], lds[a >> 2], a & 3);
+                    x = lds_bytes4(lds, j * B + L.blob_off + r);
                 } else {
-                    x = 0;
-                    for (int y = 0; y < 4; y++) {
-                        x |= lds_u8(lds, j * B + L.blob_off + r) << (8 * y);
-                        if (++r == w) { r = 0; j++; }
-                    }
+                    const uint32_t k = w - r;   // 1..3 bytes of row j, then row j + 1
+                    x = (lds_bytes4(lds, j * B + L.blob_off + r) & ((1u << (8 * k)) - 1u)) |
+                        (lds_bytes4(lds, (j + 1) * B + L.blob_off) << (8 * k));
                 }
-                if (L.flags & 1u) {
-                    x |= x >> 4; x |= x >> 2; x |= x >> 1;
-                    x &= 0x01010101u;
-                }
-                v[k] = x;
+                __builtin_nontemporal_store(x, dst + d);
             }
-            *(u32x4*)dst = v;
         } else {
-            for (uint32_t b = t0; b < R; b++) {
-                const uint32_t j = w > 1 ? __umulhi(b, L.magic) : b;
-                uint32_t x = lds_u8(lds, j * B + L.blob_off + (b - j * w));
-                if (L.flags & 1u) x = x != 0;
-                dst[b - t0] = (uint8_t)x;
+            for (uint32_t d = tid; d < D; d += kBlock) {
+                uint32_t x = 0;
+#pragma unroll
+                for (int y = 0; y < 4; y++) {
+                    const uint32_t b = 4 * d + y;
+                    const uint32_t j = w > 1 ? __umulhi(b, L.magic) : b;
+                    uint32_t v = lds_u8(lds, j * B + L.blob_off + (b - j * w));
+                    if (L.flags & 1u) v = v != 0;
+                    x |= v << (8 * y);
+                }
+                __builtin_nontemporal_store(x, dst + d);
             }
+        }
+        // ragged tail (R % 4 bytes, last tile only)
+        for (uint32_t b = 4 * D + tid; b < R; b += kBlock) {
+            const uint32_t j = w > 1 ? __umulhi(b, L.magic) : b;
+            uint32_t v = lds_u8(lds, j * B + L.blob_off + (b - j * w));
+            if (L.flags & 1u) v = v != 0;
+            L.dst[blob0 * w + b] = (uint8_t)v;
         }
     }
     // 4. validity (every node is present in the canonical layout)
@@ -2364,7 +2393,8 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
     for (const DecFix& f : s->dfix) fast = fast && ((uintptr_t)dc.data[f.col] & 15) == 0;
     if (fast) {
         const uint32_t T = (uint32_t)s->fix_T, QW = (uint32_t)((B + 3) / 4);
-        const size_t lds = (size_t)T * B + 16 + 8 * QW + 4 * ((T + 1) & ~1u) + 32 * s->dfix.size();
+        const size_t lds = (size_t)T * B + 16 + 8 * QW + 4 * ((T + 1) & ~1u) + sizeof(LDec) * s->dfix.size() +
+                           4 * (QW + 2);
         hipLaunchKernelGGL(k_decode_fixed, dim3((unsigned)((n + T - 1) / T)), dim3(kBlock), lds, st, t->dfix, t->dec,
                            dc, arena, offsets, (uint64_t)n, status);
     } else if (getenv("PACKOS_DECODE_NOWIN")) {
