@@ -1516,14 +1516,20 @@ __global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols col
 //      the staged blobs (funnel-shifted dword reads; bools normalised);
 //   4. mark validity, then run decode_blob for the (rare) blobs that failed
 //      the check, overwriting their rows with the exact reference behaviour.
-struct LDec {                 // LDS copy of a DecFix with its output column resolved
-    uint8_t* dst;
-    uint32_t width, blob_off, flags, magic, unit_begin, pad;
+// The fixed columns with their output pointers resolved, built on the host
+// per call and passed as a kernel argument: the column walk reads it with a
+// uniform index (scalar loads), so no dependent table load sits in front of
+// the first barrier.
+constexpr int kDecK = 24;
+struct DecColsK {
+    uint8_t* dst[kDecK];
+    uint32_t width[kDecK], blob_off[kDecK], flags[kDecK], magic[kDecK];
+    int32_t n;
 };
 
 __device__ __forceinline__ uint32_t lds_u8(const uint32_t* lds, uint32_t a) { return (lds[a >> 2] >> (8 * (a & 3))) & 0xFFu; }
 
-__global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecProgram P, DecCols cols,
+__global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecProgram P, DecCols cols, DecColsK K,
                                                          const uint8_t* __restrict__ arena,
                                                          const uint64_t* __restrict__ offs, uint64_t n,
                                                          uint32_t* __restrict__ status) {
@@ -1535,7 +1541,6 @@ __global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecPro
     const int tid = threadIdx.x;
     uint32_t* chk = lds + (T * B / 4 + 4);
     uint32_t* fail = chk + 2 * QW;
-    LDec* ltab = (LDec*)(fail + ((T + 1) & ~1u));
 
     // the tile base is one scalar load; whether the tile's blobs really lie
     // back to back at stride B is checked while the staging DMA is in flight
@@ -1545,12 +1550,6 @@ __global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecPro
     bool ok = true;
     for (uint32_t q = tid; q < 2 * QW; q += kBlock) chk[q] = F.chk[q];
     for (uint32_t j = tid; j < rows; j += kBlock) fail[j] = 0;
-    if (tid < kWave)   // uniform item walk: EncCols/DecCols are kernel arguments (no lane-indexed reads)
-        for (int c = 0; c < F.n_cols; c++) {
-            const DecFix fc = F.cols[c];
-            const LDec x{cols.data[fc.col], fc.width, fc.blob_off, fc.flags, fc.magic, fc.unit_begin, 0};
-            if (tid == 0) ltab[c] = x;
-        }
     // 1. stage: global -> LDS with global_load_lds_dwordx4 (every chunk of the
     //    tile in flight at once; a load -> ds_write loop waits per chunk)
     const uint32_t bytes = rows * B;
@@ -1576,7 +1575,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecPro
     }
     // 2. constant-byte check, over the blob dwords that HOLD constant bytes
     //    (header words, literals: 5 of 64 for metric M), compacted by ballot
-    uint32_t* cq = fail + ((T + 1) & ~1u) + ((sizeof(LDec) * F.n_cols + 3) >> 2);  // after ltab
+    uint32_t* cq = fail + ((T + 1) & ~1u);
     if (tid < kWave) {
         uint32_t nq = 0;
         for (uint32_t q0 = 0; q0 < QW; q0 += kWave) {
@@ -1602,9 +1601,9 @@ __global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecPro
     }
     // 3. columns: uniform walk over the columns; threads stride the column's
     //    output dwords (consecutive lanes -> consecutive dwords: 256-B stores)
-    for (int c = 0; c < F.n_cols; c++) {
-        const LDec L = ltab[c];
-        const uint32_t w = L.width, R = rows * w, D = R >> 2;
+    for (int c = 0; c < K.n; c++) {
+        struct { uint8_t* dst; uint32_t blob_off, flags, magic; } L = {K.dst[c], K.blob_off[c], K.flags[c], K.magic[c]};
+        const uint32_t w = K.width[c], R = rows * w, D = R >> 2;
         uint32_t* dst = (uint32_t*)(L.dst + blob0 * w);   // 4-B aligned: T*w % 4 == 0, base 16-B aligned
         if ((w & 3) == 0) {
             for (uint32_t d = tid; d < D; d += kBlock) {
@@ -2391,12 +2390,23 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
     bool fast = s->dec_fast == 1 && ((uintptr_t)arena & 15) == 0 && (offsets || stride == (uint64_t)B) &&
                 !getenv("PACKOS_DECODE_GENERIC");
     for (const DecFix& f : s->dfix) fast = fast && ((uintptr_t)dc.data[f.col] & 15) == 0;
+    fast = fast && s->dfix.size() <= (size_t)kDecK;
     if (fast) {
         const uint32_t T = (uint32_t)s->fix_T, QW = (uint32_t)((B + 3) / 4);
-        const size_t lds = (size_t)T * B + 16 + 8 * QW + 4 * ((T + 1) & ~1u) + sizeof(LDec) * s->dfix.size() +
-                           4 * (QW + 2);
+        const size_t lds = (size_t)T * B + 16 + 8 * QW + 4 * ((T + 1) & ~1u) + 4 * (QW + 2);
+        DecColsK K;
+        memset(&K, 0, sizeof(K));
+        K.n = (int32_t)s->dfix.size();
+        for (int c = 0; c < K.n; c++) {
+            const DecFix& f = s->dfix[c];
+            K.dst[c] = dc.data[f.col];
+            K.width[c] = f.width;
+            K.blob_off[c] = f.blob_off;
+            K.flags[c] = f.flags;
+            K.magic[c] = f.magic;
+        }
         hipLaunchKernelGGL(k_decode_fixed, dim3((unsigned)((n + T - 1) / T)), dim3(kBlock), lds, st, t->dfix, t->dec,
-                           dc, arena, offsets, (uint64_t)n, status);
+                           dc, K, arena, offsets, (uint64_t)n, status);
     } else if (getenv("PACKOS_DECODE_NOWIN")) {
         hipLaunchKernelGGL(k_decode, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, t->dec, dc,
                            arena, offsets, stride, (uint64_t)n, status);
