@@ -419,8 +419,11 @@ struct Builder {
                     cv |= (uint32_t)bm[4 * q + b].val << (8 * b);
                     s->canon[4 * q + b] = bm[4 * q + b].val;
                 }
-            s->dchk.push_back(cm);
-            s->dchk.push_back(cv);
+            if (cm) {   // compact: only the dwords that hold constant bytes
+                s->dchk.push_back((uint32_t)q);
+                s->dchk.push_back(cm);
+                s->dchk.push_back(cv);
+            }
         }
         s->dfix.clear();
         uint32_t units = 0;

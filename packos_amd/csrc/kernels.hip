@@ -1540,7 +1540,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecPro
     const uint32_t rows = (uint32_t)min((uint64_t)T, n - blob0);
     const int tid = threadIdx.x;
     uint32_t* chk = lds + (T * B / 4 + 4);
-    uint32_t* fail = chk + 2 * QW;
+    uint32_t* fail = chk + 3 * QW;
 
     // the tile base is one scalar load; whether the tile's blobs really lie
     // back to back at stride B is checked while the staging DMA is in flight
@@ -1548,7 +1548,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecPro
     const uint64_t base = offs ? ((c_u64*)(uintptr_t)offs)[blob0] : blob0 * B;
     const bool aligned_base = (base & 15) == 0;
     bool ok = true;
-    for (uint32_t q = tid; q < 2 * QW; q += kBlock) chk[q] = F.chk[q];
+    for (uint32_t q = tid; q < 3u * (uint32_t)F.n_chk; q += kBlock) chk[q] = F.chk[q];
     for (uint32_t j = tid; j < rows; j += kBlock) fail[j] = 0;
     // 1. stage: global -> LDS with global_load_lds_dwordx4 (every chunk of the
     //    tile in flight at once; a load -> ds_write loop waits per chunk)
@@ -1574,29 +1574,16 @@ __global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecPro
         return;
     }
     // 2. constant-byte check, over the blob dwords that HOLD constant bytes
-    //    (header words, literals: 5 of 64 for metric M), compacted by ballot
-    uint32_t* cq = fail + ((T + 1) & ~1u);
-    if (tid < kWave) {
-        uint32_t nq = 0;
-        for (uint32_t q0 = 0; q0 < QW; q0 += kWave) {
-            const uint32_t q = q0 + tid;
-            const bool has = q < QW && chk[2 * q] != 0u;
-            const uint64_t m = __ballot(has);
-            if (has) cq[1 + nq + __popcll(m & ((1ull << tid) - 1))] = q;
-            nq += __popcll(m);
-        }
-        if (tid == 0) cq[0] = nq;
-    }
-    __syncthreads();
+    //    (header words, literals: 5 of 64 for metric M; list built at compile)
     {
-        const uint32_t nq = cq[0];
+        const uint32_t nq = (uint32_t)F.n_chk;
         const uint32_t nq_magic = nq > 1 ? (uint32_t)((0x100000000ull + nq - 1) / nq) : 0u;
         for (uint32_t e = tid; e < rows * nq; e += kBlock) {
             const uint32_t j = nq > 1 ? __umulhi(e, nq_magic) : e;
-            const uint32_t q = cq[1 + e - j * nq];
-            const uint32_t a = j * B + 4 * q;   // blob dword q (B % 4 == 0: aligned)
+            const uint32_t* c = chk + 3 * (e - j * nq);
+            const uint32_t a = j * B + 4 * c[0];   // blob dword q (B % 4 == 0: aligned)
             const uint32_t v = (B & 3) == 0 ? lds[a >> 2] : lds_bytes4(lds, a);
-            if ((v & chk[2 * q]) != chk[2 * q + 1]) fail[j] = 1;
+            if ((v & c[1]) != c[2]) fail[j] = 1;
         }
     }
     // 3. columns: uniform walk over the columns; threads stride the column's
@@ -1869,6 +1856,7 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     t.dec.n_lits = (int32_t)s->lits.size();
     t.dfix.cols = (const DecFix*)(b + o_dfix);
     t.dfix.chk = (const uint32_t*)(b + o_dchk);
+    t.dfix.n_chk = (int32_t)(s->dchk.size() / 3);
     t.dfix.B = (int)s->all_present_size;
     t.dfix.T = s->fix_T;
     t.dfix.n_cols = (int)s->dfix.size();
@@ -2393,7 +2381,7 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
     fast = fast && s->dfix.size() <= (size_t)kDecK;
     if (fast) {
         const uint32_t T = (uint32_t)s->fix_T, QW = (uint32_t)((B + 3) / 4);
-        const size_t lds = (size_t)T * B + 16 + 8 * QW + 4 * ((T + 1) & ~1u) + 4 * (QW + 2);
+        const size_t lds = (size_t)T * B + 16 + 12 * QW + 4 * ((T + 1) & ~1u);
         DecColsK K;
         memset(&K, 0, sizeof(K));
         K.n = (int32_t)s->dfix.size();

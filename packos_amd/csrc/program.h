@@ -173,11 +173,12 @@ struct DecFix {
 
 struct DecFixProgram {
     const DecFix* cols;
-    const uint32_t* chk;   // ceil(B/4) pairs {constant-byte mask, constant value}
+    const uint32_t* chk;   // n_chk triples {blob dword q, constant-byte mask, constant value}, mask != 0
     int32_t B, T, n_cols, total_units;
     uint32_t q_magic;      // B % 4 == 0: ceil(2^32 / (B/4)) (0 when B/4 == 1)
     uint32_t b_magic;      // B % 4 != 0: ceil(2^32 / B)
     int32_t n_all_cols;    // every schema column (validity marking)
+    int32_t n_chk;
 };
 
 // column pointer tables passed by value as kernel arguments
