@@ -100,8 +100,8 @@ def main():
     total_out = r.total
     out = r.arena
 
-    # one step = one plan replay: fixed -> one encode launch; var -> size pass +
-    # scan + encode, all on `stream`, no host sync
+    # one step = one plan replay: fixed -> one encode launch; var -> size kernel
+    # + encode kernel, all on `stream`, no host sync
     plan = EncodePlan(schema, dcols, out=out, stream=stream)
     step = plan.run
 

@@ -211,8 +211,8 @@ class EncodePlan:
     """Pre-bound encode of one batch into a preallocated arena: run() issues
     only C-ABI calls on `stream` (no host sync, no allocation) — what a serving
     loop or a graph capture replays.  Fixed-size batches: one encode call.
-    Variable-size batches: one packos_encode_batch call (sizes, look-back scan
-    and encode in a single kernel); the arena is sized once at construction
+    Variable-size batches: one packos_encode_batch call (size kernel with a
+    look-back scan, then the encode kernel); the arena is sized once at construction
     (one host sync there) and `offsets` / `status` are refreshed by every
     run()."""
 
@@ -257,8 +257,8 @@ class EncodePlan:
             check(L.packos_encode_batch(self.schema.handle, self._arr, n, self.out.data_ptr(), self.out.numel(),
                                         None, stp, None, 0, self.flags, st), "packos_encode_batch")
             return self.out
-        # one call: the single-pass kernel computes sizes, scans them (look-back)
-        # and encodes; `offsets` is rewritten by every run
+        # one call: the size kernel (sizes + look-back scan -> offsets) and the
+        # encode kernel; `offsets` is rewritten by every run
         check(L.packos_encode_batch(self.schema.handle, self._arr, n, self.out.data_ptr(), self.out.numel(),
                                     self.offsets.data_ptr(), stp, self.ws.data_ptr(), self.wsb,
                                     self.flags, st), "packos_encode_batch")

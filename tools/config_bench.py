@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-config GPU vs CPU rates: for every BASELINE config,
-device-resident encode (EncodePlan replay: for var schemas one single-pass
-encode call) and decode (DecodeBuffer semantics) on cuda:0, the CPU oracle
+device-resident encode (EncodePlan replay: for var schemas the size kernel +
+the encode kernel) and decode (DecodeBuffer semantics) on cuda:0, the CPU oracle
 (C restatement of the reference, 'port') on the host cores over a bounded
 sample, the speed-ups, and for var configs a chunked pinned
 H2D + encode + D2H rate.  One JSON line per config.
@@ -27,7 +27,10 @@ import oracle_bridge as ob  # noqa: E402  (CPU baseline only)
 GPU_N = {"C1": 1000, "C2": 1 << 20, "C3": 1 << 20, "C4": 1 << 22, "C5": 1 << 21, "M": 1 << 20}
 
 
-def tmed(fn, reps):
+def tmed(fn, reps, group=10):
+    """Median over `reps` groups of `group` back-to-back calls, one HIP event
+    pair per group (a timing event record costs ~9 us of GPU time on the box,
+    tools/hostcost.py — one pair per call would inflate short kernels)."""
     st = torch.cuda.current_stream()
     fn()
     torch.cuda.synchronize()
@@ -35,10 +38,11 @@ def tmed(fn, reps):
     for _ in range(reps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(st)
-        fn()
+        for _ in range(group):
+            fn()
         b.record(st)
         torch.cuda.synchronize()
-        ts.append(a.elapsed_time(b))
+        ts.append(a.elapsed_time(b) / group)
     return float(np.median(ts))
 
 
@@ -74,8 +78,8 @@ def cpu_rates(cfg, n, seconds):
 
 
 def e2e_var(schema, hc, plan_total, reps=1):
-    """Chunked pinned H2D (columns) + single-pass encode + D2H (arena), two
-    streams double-buffered.  Offsets per chunk come from the encode kernel;
+    """Chunked pinned H2D (columns) + size kernel + encode kernel + D2H (arena),
+    two streams double-buffered.  Offsets per chunk come from the size kernel;
     the D2H byte count from the host-side layout (flat chains: base + var)."""
     from packos_amd import _lib
     L = _lib.lib()
@@ -158,7 +162,7 @@ def e2e_var(schema, hc, plan_total, reps=1):
     el = (time.perf_counter() - t0) / reps
     ok = bool(int(boff[-1]) == plan_total)
     return {"million_blobs_per_s": round(n / el / 1e6, 3), "gib_per_s_out": round(int(boff[-1]) / el / 2 ** 30, 3),
-            "chunks": nch, "size_check": ok, "note": "pinned H2D + single-pass encode + D2H, 2 streams"}, out_host
+            "chunks": nch, "size_check": ok, "note": "pinned H2D + size kernel + encode kernel + D2H, 2 streams"}, out_host
 
 
 def main():
@@ -178,6 +182,7 @@ def main():
         torch.cuda.synchronize()
         fixed = plan.fixed
         enc_ms = tmed(plan.run, args.reps)
+        enc_ms1 = tmed(plan.run, args.reps, group=1)
         alg_enc = algorithmic_bytes(hc, plan.total, with_offsets=not fixed)
         offs = plan.offsets
         stride = 0 if offs is not None else s.fixed_blob_size
@@ -187,6 +192,8 @@ def main():
         torch.cuda.synchronize()
         bad = int((st != 0).sum().item())
         dec_ms = tmed(lambda: decode_batch(s, plan.out, offs, n, stride=stride, out=out, status=st), args.reps)
+        dec_ms1 = tmed(lambda: decode_batch(s, plan.out, offs, n, stride=stride, out=out, status=st), args.reps,
+                       group=1)
         vals = sum(n * sp.width for sp in s.specs if sp.fixed) + sum(12 * n for sp in s.specs if sp.var)
         # var values are returned as (start, length) views into the arena
         # (GetBytes / GetStringUnsafe aliasing): their bytes are never read
@@ -196,11 +203,13 @@ def main():
         g_enc = n / enc_ms / 1e3
         g_dec = n / dec_ms / 1e3
         line = {"config": name, "note": cfg.note, "n_gpu": n, "blob_bytes_mean": round(plan.total / n, 1),
-                "encode": {"ms": round(enc_ms, 4), "million_blobs_per_s": round(g_enc, 2),
+                "encode": {"ms": round(enc_ms, 4), "ms_one_event_pair_per_call": round(enc_ms1, 4),
+                           "million_blobs_per_s": round(g_enc, 2),
                            "GBps_algorithmic": round(alg_enc / enc_ms / 1e6, 1),
                            "roofline_frac": round(alg_enc / enc_ms / 1e6 / 8000.0, 4),
-                           "includes": "encode" if fixed else "single-pass encode (sizes + look-back scan + encode)"},
-                "decode": {"ms": round(dec_ms, 4), "million_blobs_per_s": round(g_dec, 2),
+                           "includes": "encode" if fixed else "size kernel (look-back scan) + encode kernel"},
+                "decode": {"ms": round(dec_ms, 4), "ms_one_event_pair_per_call": round(dec_ms1, 4),
+                           "million_blobs_per_s": round(g_dec, 2),
                            "GBps_algorithmic": round(alg_dec / dec_ms / 1e6, 1),
                            "fast_path": s.decode_fast, "nonzero_status": bad},
                 "cpu_oracle": {"encode_million_blobs_per_s": round(cpu["encode"] / 1e6, 3),

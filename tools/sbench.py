@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Var-size encode A/B: single-pass k_encode_stream (EncodePlan.run, one call)
+"""Var-size encode A/B: k_stream_sizes + k_encode_stream (EncodePlan.run, one call)
 vs the two-kernel tiled encoder (PACKOS_VAR_KERNEL=tile: size pass + scan +
 tile kernel), same process, interleaved; outputs must be byte-equal.
 
