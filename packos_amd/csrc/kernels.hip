@@ -1481,26 +1481,52 @@ __global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols col
     for (int x = tid; x < P.n_nodes; x += kBlock) lnodes[x] = P.nodes[x];
     for (int x = tid; x < P.n_kids; x += kBlock) lkids[x] = P.kids[x];
     for (int x = tid; x < P.n_lits; x += kBlock) llits[x] = P.lits[x];
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + tid;
+    const uint64_t lo = (uint64_t)blockIdx.x * kBlock, i = lo + tid;
+    const uint32_t rows = (uint32_t)min((uint64_t)kBlock, n - lo);
     uint64_t a0 = 0, a1 = 0;
     if (i < n) {
         a0 = offs ? offs[i] : i * stride;
         a1 = offs ? offs[i + 1] : (i + 1) * stride;
     }
-    uint8_t* w = win + tid * kDecWinChunks * 16;
-    const uint64_t b0 = a0 & ~15ull;
-    const uint64_t end = min(a1, b0 + 16ull * kDecWinChunks);
-    const uint32_t nch = (i < n && end > a0) ? (uint32_t)((end - b0 + 15) >> 4) : 0u;
-    u32x4 v[kDecWinChunks];
+    // Small blobs: when the tile's whole byte range fits the window memory,
+    // stage it once with coalesced LDS-DMA and let every blob read from there
+    // (same reader, one shared window).  Otherwise each blob's first
+    // kDecWinChunks * 16 bytes go to its own window (headers + fixed fields sit
+    // at the front; var values are returned as views and never read).
+    typedef __attribute__((address_space(4))) const uint64_t c_u64;
+    const uint64_t t0 = offs ? ((c_u64*)(uintptr_t)offs)[lo] : lo * stride;
+    const uint64_t t1 = offs ? ((c_u64*)(uintptr_t)offs)[lo + rows] : (lo + rows) * stride;
+    const uint64_t tb = t0 & ~15ull;
+    const bool tile_mode = t1 >= t0 && t1 - tb <= (uint64_t)sizeof(win) && ((uintptr_t)arena & 15) == 0;
+    uint8_t* w;
+    uint64_t b0;
+    uint32_t wbytes;
+    if (tile_mode) {
+        const uint32_t nch = (uint32_t)((t1 - tb + 15) >> 4), lane = tid & 63, c00 = tid & ~63u;
+        const uint32_t lds0 = (uint32_t)(uintptr_t)win;
+        for (uint32_t c0 = c00; c0 < nch; c0 += kBlock)
+            if (c0 + lane < nch) dma16(arena + tb + 16u * (c0 + lane), __builtin_amdgcn_readfirstlane(lds0 + 16u * c0));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        w = win;
+        b0 = tb;
+        wbytes = 16 * nch;
+    } else {
+        w = win + tid * kDecWinChunks * 16;
+        b0 = a0 & ~15ull;
+        const uint64_t end = min(a1, b0 + 16ull * kDecWinChunks);
+        const uint32_t nch = (i < n && end > a0) ? (uint32_t)((end - b0 + 15) >> 4) : 0u;
+        u32x4 v[kDecWinChunks];
 #pragma unroll
-    for (int c = 0; c < kDecWinChunks; c++)
-        if ((uint32_t)c < nch) v[c] = *(const g_u32x4*)(arena + b0 + 16 * c);
+        for (int c = 0; c < kDecWinChunks; c++)
+            if ((uint32_t)c < nch) v[c] = *(const g_u32x4*)(arena + b0 + 16 * c);
 #pragma unroll
-    for (int c = 0; c < kDecWinChunks; c++)
-        if ((uint32_t)c < nch) *(u32x4*)(w + 16 * c) = v[c];
+        for (int c = 0; c < kDecWinChunks; c++)
+            if ((uint32_t)c < nch) *(u32x4*)(w + 16 * c) = v[c];
+        wbytes = 16 * nch;
+    }
     __syncthreads();
     if (i >= n) return;
-    const WReader R{arena, w, b0, 16 * nch};
+    const WReader R{arena, w, b0, wbytes};
     const DecProgram LP{lnodes, lkids, llits, P.root, P.n_nodes, P.n_kids, P.n_lits};
     status[i] = decode_blob(LP, cols, R, a0, a1, i);
 }

@@ -44,7 +44,9 @@ for name in sys.argv[1:] or ["M", "C2", "C4", "C3"]:
     bad = int((st != 0).sum().item())
     ms = tmed(lambda: decode_batch(s, r.arena, offs, n, out=out, status=st))
     vals = sum(n * sp.width for sp in s.specs if sp.fixed) + sum(12 * n for sp in s.specs if sp.var)
-    alg = r.total + 8 * n + vals + 4 * n
+    # var values come back as views into the arena: their bytes are not read
+    var_bytes = sum(int(hc.offsets[c][-1]) for c, sp in enumerate(hc.specs) if sp.var)
+    alg = r.total - var_bytes + 8 * n + vals + 4 * n
     extra = {}
     if r.offsets is None:   # fixed-size batch: also by stride (no offsets array)
         extra["decode_stride_ms"] = round(tmed(lambda: decode_batch(s, r.arena, None, n, out=out, status=st,
