@@ -108,6 +108,36 @@ def test_random_schema_encode_stream_knobs(seed, knobs, monkeypatch):
     assert_same_encoding(chain, hc, seed % 2, f"knobs {knobs} seed {seed}", fused=True)
 
 
+@pytest.mark.parametrize("fields,tuples,nest", [(43, 0, 0), (44, 0, 0), (45, 0, 0), (60, 0, 0), (6, 15, 0),
+                                               (6, 16, 0), (6, 0, 12)])
+def test_stream_plan_limits(fields, tuples, nest):
+    """Schemas at and past the stream encoder's plan limits (48 items, 16
+    containers): past them the call routes to the tiled encoder; both must
+    match the oracle.  Items = one header block per container + the leaves:
+    `fields` flat leaves, `tuples` one-leaf tuples (one container each), and a
+    tuple nested `nest` deep (12 is the compiler's depth limit)."""
+    import random
+    rng = random.Random(fields * 31 + tuples * 7 + nest)
+    leaves = [SInt16 if k % 3 else SVariableString() for k in range(fields)]
+    tups = [STuple(SVariableString()) for _ in range(tuples)]
+    node = STuple(SInt16, SVariableString())
+    for _ in range(nest):   # a chain of tuples inside tuples
+        node = STuple(SInt16, node)
+    chain = SChain(*leaves, *tups, node)
+    rows = []
+    for i in range(600):
+        r = [rng.getrandbits(16) if k % 3 else "v" * rng.randint(0, 90) for k in range(fields)]
+        t = [["t" * rng.randint(0, 60)] for _ in range(tuples)]
+        inner = [rng.getrandbits(16), "w" * rng.randint(0, 70)]
+        for _ in range(nest):
+            inner = [rng.getrandbits(16), inner]
+        rows.append(r + t + [inner])
+    hc = HostColumns.from_rows(chain, rows)
+    for mode in (0, 1):
+        assert_same_encoding(chain, hc, mode, f"fields {fields} nest {nest} mode {mode}")
+        assert_same_encoding(chain, hc, mode, f"fields {fields} nest {nest} mode {mode} fused", fused=True)
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("seed", range(20))
 def test_random_schema_encode_tile_kernel(seed, mode, monkeypatch):
