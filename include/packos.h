@@ -221,6 +221,24 @@ int packos_encode_batch(const packos_schema* s, const packos_column* cols, size_
                         uint32_t* status, void* workspace, size_t workspace_bytes,
                         uint32_t flags, void* stream);
 
+/* ---- host-resident batches ------------------------------------------------ */
+
+/* Encode n blobs whose columns live in HOST memory into a host arena — the
+ * entry point a cgo / JNI shim calls for RPC payloads or BadgerDB values
+ * (PackAppend / Pack per blob, access/put.go:619-681, for a whole batch).
+ * Chunks of `chunk_blobs` blobs (0 = 1M) move through device buffers on two
+ * streams of the current device: hipMemcpyAsync H2D, the size kernel + encode
+ * kernel (or the fixed-layout kernel), D2H; one chunk's copies overlap the
+ * other's kernels.  Pinned host buffers (hipHostMalloc / hipHostRegister)
+ * make the copies asynchronous; pageable ones work too.  host_cols use the
+ * same layout as packos_encode_batch's device columns.  host_offsets (n+1)
+ * receives the blob starts (required for variable-size batches); host_status
+ * (n) may be NULL.  Blocks until done.  Returns PACKOS_E_CAPACITY when the
+ * output exceeds out_capacity (n * static size + all var bytes always fits). */
+int packos_encode_host_batch(const packos_schema* s, const packos_column* host_cols, size_t n_blobs,
+                             uint8_t* host_out, uint64_t out_capacity, uint64_t* host_offsets,
+                             uint32_t* host_status, size_t chunk_blobs);
+
 /* ---- batch decode (schema.DecodeBuffer semantics) ------------------------- */
 
 /* blob i = arena[offsets[i] .. offsets[i+1]); offsets == NULL means fixed

@@ -207,6 +207,49 @@ def encode_batch(schema: CompiledSchema, cols: DeviceColumns, want_offsets: bool
     return EncodeResult(out, offs, status[:n] if status is not None else None, total, -1)
 
 
+def host_batch_bound(schema: CompiledSchema, hc: HostColumns) -> int:
+    """Output bytes that always suffice: every non-var item present in every
+    blob + all var bytes."""
+    L = lib()
+    ncol = len(schema.specs)
+    widths = np.zeros(max(1, ncol), dtype=np.uint32)
+    valid = np.ones(max(1, ncol), dtype=np.uint8)
+    stat = int(L.packos_schema_blob_size_host(schema.handle, widths.ctypes.data, valid.ctypes.data))
+    var_bytes = sum(int(o[hc.n]) - int(o[0]) for o in hc.offsets if o is not None)
+    return max(16, hc.n * max(stat, 0) + var_bytes)
+
+
+def encode_host_batch(schema: CompiledSchema, hc: HostColumns, chunk_blobs: int = 0,
+                      want_status: bool = True, out=None, offsets=None, status=None):
+    """Host-resident batch -> host arena through packos_encode_host_batch
+    (chunked H2D / encode / D2H on two streams of the current device; the
+    entry point a cgo shim binds).  `out` / `offsets` / `status` may be
+    preallocated numpy arrays (e.g. views of pinned memory).  Returns
+    (arena, offsets, status); arena is trimmed to the encoded bytes."""
+    L = lib()
+    n = hc.n
+    keep = []
+    arr = (PackosColumn * max(1, len(schema.specs)))()
+    for c in range(len(schema.specs)):
+        for name, attr in (("data", "data"), ("offsets", "offsets"), ("valid", "valid")):
+            a = getattr(hc, attr)[c]
+            if a is None:
+                continue
+            a = np.ascontiguousarray(a)
+            keep.append(a)
+            setattr(arr[c], name, a.ctypes.data)
+    if out is None:
+        out = np.empty(host_batch_bound(schema, hc), dtype=np.uint8)
+    cap = out.size
+    offs = offsets if offsets is not None else np.empty(n + 1, dtype=np.uint64)
+    st = status if status is not None else (np.empty(max(n, 1), dtype=np.uint32) if want_status else None)
+    check(L.packos_encode_host_batch(schema.handle, arr, n, out.ctypes.data, cap, offs.ctypes.data,
+                                     None if st is None else st.ctypes.data, chunk_blobs),
+          "packos_encode_host_batch")
+    del keep
+    return out[: int(offs[n])], offs, (st[:n] if st is not None else None)
+
+
 class EncodePlan:
     """Pre-bound encode of one batch into a preallocated arena: run() issues
     only C-ABI calls on `stream` (no host sync, no allocation) — what a serving

@@ -138,6 +138,41 @@ def test_stream_plan_limits(fields, tuples, nest):
         assert_same_encoding(chain, hc, mode, f"fields {fields} nest {nest} mode {mode} fused", fused=True)
 
 
+@pytest.mark.parametrize("name,n,chunk,pinned", [("C3", 20000, 3000, False), ("C3", 20000, 0, True),
+                                                 ("M", 10001, 4096, False), ("M", 10001, 4096, True),
+                                                 ("C5", 3000, 700, False), ("C1", 1000, 0, False),
+                                                 ("C4", 5001, 1024, True), ("C2", 7777, 1000, False)])
+def test_encode_host_batch(name, n, chunk, pinned):
+    """packos_encode_host_batch (host columns -> chunked H2D / encode / D2H on
+    two streams -> host arena) vs the oracle, pageable and pinned inputs,
+    many chunks (both pipeline slots reused)."""
+    from packos_amd.api import encode_host_batch
+    T = torch()
+    cfg = CONFIGS[name]
+    hc = make_columns(cfg, n=n)
+    if pinned:
+        for lst in (hc.data, hc.offsets, hc.valid):
+            for c, a in enumerate(lst):
+                if a is not None:
+                    lst[c] = T.from_numpy(np.ascontiguousarray(a)).pin_memory().numpy()
+    s = CompiledSchema(cfg.chain, cfg.mode)
+    a1, o1, s1 = encode_host_batch(s, hc, chunk_blobs=chunk)
+    a0, o0, s0 = ob.encode(cfg.chain, hc, cfg.mode, nthreads=8)
+    assert np.array_equal(o0, o1) and np.array_equal(a0, a1) and np.array_equal(s0, s1.astype(np.uint32))
+
+
+@pytest.mark.parametrize("seed", range(0, 60, 5))
+def test_encode_host_batch_random(seed):
+    from packos_amd.api import encode_host_batch
+    chain = rand_chain(seed)
+    hc = HostColumns.from_rows(chain, rand_rows(chain, 2500, seed * 3 + 2))
+    for mode in (0, 1):
+        s = CompiledSchema(chain, mode)
+        a1, o1, s1 = encode_host_batch(s, hc, chunk_blobs=600)
+        a0, o0, s0 = ob.encode(chain, hc, mode, nthreads=8)
+        assert np.array_equal(o0, o1) and np.array_equal(a0, a1) and np.array_equal(s0, s1.astype(np.uint32))
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("seed", range(20))
 def test_random_schema_encode_tile_kernel(seed, mode, monkeypatch):
