@@ -1940,6 +1940,30 @@ static int size_pass(packos_schema* s, DeviceTables* t, const EncCols& ec, size_
         HIP_TRY(hipMemsetAsync(offs, 0, sizeof(uint64_t), st));
         return PACKOS_OK;
     }
+    // data-independent presence: closed-form sizes (k_sizes_affine), no scan
+    {
+        AffPlan A{};
+        bool affine = getenv("PACKOS_SIZES_SCAN") == nullptr;
+        for (const EncCont& c : s->conts) affine &= c.valid_col < 0 || ec.valid[c.valid_col] == nullptr;
+        for (const EncItem& it : s->items) {
+            if (!affine) break;
+            if (it.type == IT_VAR) {
+                if (A.nv == kAffVar) affine = false;
+                else A.off[A.nv++] = ec.off[it.col];
+            } else {
+                if (it.type == IT_FIXED && it.nullable && ec.valid[it.col] && s->mode != PACKOS_MODE_PACKABLE)
+                    affine = false;
+                A.C += it.size;
+            }
+        }
+        if (affine) {
+            const uint64_t per = (uint64_t)kBlock * kAffPer;
+            hipLaunchKernelGGL(k_sizes_affine, dim3((unsigned)((n + 1 + per - 1) / per)), dim3(kBlock), 0, st, A,
+                               offs, (uint64_t)n);
+            HIP_TRY(hipGetLastError());
+            return PACKOS_OK;
+        }
+    }
     // k_stream_sizes: ticket + per-tile look-back words at the start of ws
     const uint64_t ntiles = (n + kSzTile - 1) / kSzTile;
     HIP_TRY(hipMemsetAsync(ws, 0, (ntiles + 1) * sizeof(uint64_t), st));

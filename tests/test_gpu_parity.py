@@ -98,6 +98,37 @@ def test_random_schema_encode(seed, mode, fused):
     assert_same_encoding(chain, hc, mode, f"seed {seed}", fused=fused)
 
 
+@pytest.mark.parametrize("scan", [False, True], ids=["closed_form", "lookback"])
+@pytest.mark.parametrize("n,seed", [(0, 1), (1, 2), (1023, 3), (1024, 4), (1025, 5), (5000, 6), (70001, 7)])
+def test_size_pass_var_base_and_counts(n, seed, scan, monkeypatch):
+    """Size pass for data-independent presence (k_sizes_affine:
+    offs[i] = i*C + sum_v off_v[i] - off_v[0]) vs the look-back scan
+    (PACKOS_SIZES_SCAN): var columns whose offsets start past 0 (a column
+    slice), block-boundary counts; offsets and bytes equal the oracle's."""
+    T = torch()
+    if scan:
+        monkeypatch.setenv("PACKOS_SIZES_SCAN", "1")
+    chain = SChain(SInt16, SVariableString(), SStringLen(5), SVariableString(), STuple(SInt16, SVariableString()))
+    rng = np.random.default_rng(seed)
+    rows = [[int(rng.integers(-30000, 30000)), "x" * int(rng.integers(0, 60)), "abcde",
+             bytes(rng.integers(32, 127, int(rng.integers(0, 300))).astype(np.uint8)).decode(),
+             [7, "y" * int(rng.integers(0, 9))]] for _ in range(n)]
+    hc = HostColumns.from_rows(chain, rows)
+    s = CompiledSchema(chain, 0)
+    dc = DeviceColumns.from_host(s, hc, "cuda:0")
+    for c, o in enumerate(dc.offsets):
+        if o is not None:   # shift every var column by a different base
+            k = 1000 + 37 * c
+            dc.data[c] = T.cat([T.full((k,), 0xEE, dtype=T.uint8, device="cuda:0"), dc.data[c]])
+            dc.offsets[c] = o + k
+    r = encode_batch(s, dc)
+    T.cuda.synchronize()
+    a0, o0, s0 = ob.encode(chain, hc, 0, nthreads=8)
+    assert np.array_equal(r.offsets.cpu().numpy().astype(np.uint64), o0)
+    assert np.array_equal(r.arena[: r.total].cpu().numpy(), a0)
+    assert np.array_equal(r.status.cpu().numpy().astype(np.uint32), s0)
+
+
 @pytest.mark.parametrize("knobs", STREAM_KNOBS[1:], ids=lambda k: ",".join(f"{a[14:]}={b}" for a, b in k.items()))
 @pytest.mark.parametrize("seed", range(0, 60, 6))
 def test_random_schema_encode_stream_knobs(seed, knobs, monkeypatch):
