@@ -13,7 +13,7 @@ from golden_util import MODES, chain_of, load, unwrap
 from packos_amd.api import CompiledSchema, DeviceColumns, decode_batch, encode_batch, get_field_batch
 from packos_amd.columns import HostColumns
 from packos_amd.configs import CONFIGS, make_columns
-from packos_amd.schema import SChain, SInt16, SStringLen, SVariableString, STuple, SMap, SString
+from packos_amd.schema import SBool, SChain, SInt16, SInt32, SInt64, SStringLen, SVariableString, STuple, SMap, SString
 from schema_gen import rand_chain, rand_rows
 
 pytestmark = pytest.mark.gpu
@@ -511,6 +511,32 @@ def test_fixed_decode_fast_path(seed):
     if np.all(np.diff(offs.astype(np.int64)) == B):  # no nil containers: stride addressing
         st2 = assert_same_decode(chain, arena, offs, n, f"fast stride seed {seed}", stride=B)
         assert np.array_equal(st, st2)
+
+
+
+@pytest.mark.parametrize("B", [32, 64, 128, 256, 512, 1024, 48, 272])
+def test_fixed_decode_blob_sizes(B):
+    """k_decode_fixed across blob sizes (power-of-two 32..1024 B and two
+    others; tile T = 16 * floor(1024 / B) blobs): narrow columns (int16 /
+    bool / int32 / int64) next to a string filling the blob, a ragged last
+    tile, corrupted blobs in the mix, offsets and stride addressing."""
+    L = B - 2 * 6 - (2 + 1 + 4 + 8)
+    chain = SChain(SInt16, SBool, SInt32, SInt64, SStringLen(L))
+    s = CompiledSchema(chain, 0)
+    assert s.fixed_blob_size == B
+    rng = np.random.default_rng(B)
+    n = 3001
+    rows = [[int(rng.integers(-32768, 32767)), bool(rng.integers(0, 2)), int(rng.integers(-2**31, 2**31 - 1)),
+             int(rng.integers(-2**62, 2**62)), bytes(rng.integers(32, 127, L).astype(np.uint8)).decode()]
+            for _ in range(n)]
+    hc = HostColumns.from_rows(chain, rows)
+    arena, offs, _ = ob.encode(chain, hc, 0)
+    arena = arena.copy()
+    for i in np.nonzero(rng.random(n) < 0.03)[0]:
+        arena[int(offs[i]) + int(rng.integers(0, B))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    st = assert_same_decode(chain, arena, offs, n, f"B={B}")
+    st2 = assert_same_decode(chain, arena, offs, n, f"B={B} stride", stride=B)
+    assert np.array_equal(st, st2)
 
 
 @pytest.mark.parametrize("name", ["M", "C2", "C4"])
