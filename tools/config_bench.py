@@ -207,7 +207,7 @@ def main():
                            "million_blobs_per_s": round(g_enc, 2),
                            "GBps_algorithmic": round(alg_enc / enc_ms / 1e6, 1),
                            "roofline_frac": round(alg_enc / enc_ms / 1e6 / 8000.0, 4),
-                           "includes": "encode" if fixed else "size kernel (look-back scan) + encode kernel"},
+                           "includes": "encode" if fixed else "size kernel (closed-form map or look-back scan) + encode kernel"},
                 "decode": {"ms": round(dec_ms, 4), "ms_one_event_pair_per_call": round(dec_ms1, 4),
                            "million_blobs_per_s": round(g_dec, 2),
                            "GBps_algorithmic": round(alg_dec / dec_ms / 1e6, 1),
