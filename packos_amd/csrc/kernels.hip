@@ -8,8 +8,11 @@
 //                   key bytes + funnel-shifted column bytes) and stores them
 //                   with global_store_dwordx4.  Pure byte/integer work, HBM
 //                   bound; no MFMA.
-//   k_stream_sizes  var-size schemas: blob sizes + decoupled look-back scan
-//                   -> out_offsets (encode_stream.inc)
+//   k_sizes_affine  var-size schemas with data-independent presence: the
+//                   scan telescopes, out_offsets[i] = i*C + sum_v(off_v[i] -
+//                   off_v[0]) — a pure map (encode_stream.inc)
+//   k_stream_sizes  other var-size schemas: blob sizes + decoupled look-back
+//                   scan -> out_offsets (encode_stream.inc)
 //   k_encode_stream var-size schemas: two bulk staging rounds into LDS, two
 //                   emitters per blob into an LDS image, 16-B stores
 //                   (encode_stream.inc)
@@ -2262,8 +2265,8 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
                              : "out_offsets required for a variable-size schema");
         return PACKOS_E_INVALID;
     }
-    // default: k_stream_sizes (look-back scan; skipped when the caller's offsets
-    // are ready) + k_encode_stream.  PACKOS_VAR_KERNEL=tile selects the
+    // default: size pass (k_sizes_affine or the k_stream_sizes look-back scan;
+    // skipped when the caller's offsets are ready) + k_encode_stream.  PACKOS_VAR_KERNEL=tile selects the
     // two-kernel tiled encoder below.
     const char* vk = getenv("PACKOS_VAR_KERNEL");
     const bool want_stream = !(flags & PACKOS_ENC_FORCE_GENERIC) && !(vk && strcmp(vk, "tile") == 0);
