@@ -123,9 +123,12 @@ def main():
         step()
     ev1.record(stream)
     torch.cuda.synchronize()
+    # this rank's time ends when its GPU work has drained; the trailing
+    # barrier keeps the ranks together and the MAX over ranks below reports
+    # the slowest one (a barrier inside the clock would add its own latency)
+    el = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
