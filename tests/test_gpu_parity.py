@@ -514,12 +514,17 @@ def test_fixed_decode_fast_path(seed):
 
 
 
+@pytest.mark.parametrize("tile", [None, "1024", "49152"], ids=["tile_default", "tile_1k", "tile_48k"])
 @pytest.mark.parametrize("B", [32, 64, 128, 256, 512, 1024, 48, 272])
-def test_fixed_decode_blob_sizes(B):
+def test_fixed_decode_blob_sizes(B, tile, monkeypatch):
     """k_decode_fixed across blob sizes (power-of-two 32..1024 B and two
     others; tile T = 16 * floor(1024 / B) blobs): narrow columns (int16 /
     bool / int32 / int64) next to a string filling the blob, a ragged last
-    tile, corrupted blobs in the mix, offsets and stride addressing."""
+    tile, corrupted blobs in the mix, offsets and stride addressing; decode
+    tiles of 1 KB / 48 KB staged bytes (PACKOS_DEC_TILE_BYTES) besides the
+    default."""
+    if tile:
+        monkeypatch.setenv("PACKOS_DEC_TILE_BYTES", tile)
     L = B - 2 * 6 - (2 + 1 + 4 + 8)
     chain = SChain(SInt16, SBool, SInt32, SInt64, SStringLen(L))
     s = CompiledSchema(chain, 0)
