@@ -1,17 +1,34 @@
 #!/usr/bin/env python3
 """Device-resident bulk PackOS encode throughput (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config M|C2|C3|C4|C5] [--e2e]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config M|C2|C3|C4|C5] [--sets S]
 
-One step = one encode launch over the whole per-GPU batch with inputs already
-resident in HBM (metric config M: 1M x 256 B fixed-schema tuples per GPU).
-N>1: launched by torch.distributed.run, one rank per GPU; blobs are
-independent, so every rank encodes its own shard (seed + rank) with no data-
-path collective (weak scaling).  Rank 0 prints ONE JSON line.
+One step = one encode of this GPU's whole shard with its inputs already
+resident in HBM (metric config M: 1M x 256 B fixed-schema tuples per GPU;
+C5: one 8,388,608-blob shard of the 64M mixed batch).
+
+Batch and shards: the N ranks encode N disjoint contiguous shards of ONE
+global synthetic batch of N x (blobs per GPU) blobs (weak scaling), planned
+byte-balanced by packos_amd.shard.plan_shards; each rank generates exactly
+its slice (the generator is indexed by global blob number).  There is no
+collective on the data path: the only communication is the harness barrier
+and the max-over-ranks timing all-reduce.
+
+Cold vs warm: the timed loop rotates over S >= 3 device copies of the shard
+(distinct input columns AND output arenas, > 750 MiB for M), so no set is
+still resident in the 256 MiB Infinity Cache when it is reused; `value`,
+`ms_per_step` and `roofline` are these cold figures.  A second loop replays
+set 0 only ("warm", labelled).
+
+Rank 0 at N=1 also times the CPU oracle (a C restatement of the reference
+encoder, test infrastructure) on every host core over the same shard, and
+checks the GPU arena of the timed run against it byte for byte (`parity`).
 """
 import argparse
+import hashlib
 import json
 import os
+import platform
 import sys
 import time
 
@@ -29,44 +46,112 @@ def parse():
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="M")
-    p.add_argument("--n", type=int, default=0, help="blobs per GPU (default: the config's)")
-    p.add_argument("--e2e", action="store_true", help="also time pinned H2D + encode + D2H")
-    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    p.add_argument("--n", type=int, default=0, help="blobs per GPU (default: the config's shard)")
+    p.add_argument("--sets", type=int, default=3, help="device copies rotated in the timed loop (cold)")
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / parity leg")
+    p.add_argument("--no-host", action="store_true", help="skip the host-resident library leg")
+    p.add_argument("--no-warm", action="store_true", help="skip the warm (single-set) loop, e.g. for PMC passes")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     return p.parse_args()
 
 
-def cpu_baseline(cfg, hc, seconds):
-    """CPU oracle (a C restatement of the reference encoder, 'port') timed on
-    this host's cores over repeated passes of the rank-0 sample."""
+# ----------------------------------------------------------------- host info
+def host_info():
+    info = {"nproc": os.cpu_count() or 1}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except Exception:
+        info["affinity"] = None
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except Exception:
+        pass
+    info["cpu_model"] = model or platform.processor() or "unknown"
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, per = f.read().split()[:2]
+            if q != "max":
+                quota = round(int(q) / int(per), 2)
+        except Exception:
+            pass
+    info["cgroup_cpu_quota"] = quota
+    return info
+
+
+def cpu_leg(cfg, hc, seconds, gpu_arena, gpu_offsets):
+    """CPU oracle ('port') timed on this host's cores over the same shard
+    (bounded: `seconds` of all-core passes, half that single-threaded), and
+    the bit-exact comparison of the GPU output with the oracle's."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bridge as ob  # checker / baseline only
-    threads = max(1, min(16, os.cpu_count() or 1))
+    hi = host_info()
+    threads = max(1, min(1024, hi["affinity"] or hi["nproc"]))
     os_ = ob.OracleSchema(cfg.chain)
     keep = []
     cols = ob.make_cols(hc, keep)
     n = hc.n
-    total = ob.lib().or_encoded_size_one(ob.C.byref(os_.s), cols, 0, cfg.mode) * n \
-        if cfg.var_len is None else None
-    if total is None:
-        total = sum(ob.lib().or_encoded_size_one(ob.C.byref(os_.s), cols, i, cfg.mode) for i in range(n))
-    arena = np.empty(total, np.uint8)
+    total = int(gpu_offsets[n]) if gpu_offsets is not None else len(gpu_arena)
+    arena = np.empty(max(total, 1), np.uint8)
     offs = np.empty(n + 1, np.uint64)
     res = {}
     for label, th in (("mt", threads), ("st", 1)):
         passes, t0 = 0, time.perf_counter()
         budget = seconds if label == "mt" else seconds / 2
         while True:
-            ob.lib().or_encode_batch(ob.C.byref(os_.s), cols, n, cfg.mode, arena.ctypes.data, arena.size,
-                                     offs.ctypes.data, None, th)
+            r = ob.lib().or_encode_batch(ob.C.byref(os_.s), cols, n, cfg.mode, arena.ctypes.data, arena.size,
+                                         offs.ctypes.data, None, th)
+            assert r == total, (r, total)
             passes += 1
             el = time.perf_counter() - t0
             if el >= budget:
                 break
         res[label] = (passes * n / el, passes, el, th)
-    return res
+    same = bool(np.array_equal(arena[:total], gpu_arena[:total]))
+    if gpu_offsets is not None:
+        same = same and bool(np.array_equal(offs, gpu_offsets.astype(np.uint64)))
+    digest = hashlib.sha256(gpu_arena[:total].tobytes()).hexdigest()[:16]
+    return res, hi, same, digest, total
 
 
+def host_leg(schema, hc):
+    """packos_encode_host_batch: pinned host columns -> chunked H2D / encode /
+    D2H through the library (the entry point a cgo shim binds) -> pinned host
+    arena.  Best of 3; never `value`."""
+    import torch
+    from packos_amd.api import encode_host_batch, host_batch_bound
+    pinned = []
+    for lst in (hc.data, hc.offsets, hc.valid):
+        for c, a in enumerate(lst):
+            if a is not None:
+                t = torch.from_numpy(np.ascontiguousarray(a)).pin_memory()
+                pinned.append(t)
+                lst[c] = t.numpy()
+    cap = host_batch_bound(schema, hc)
+    out = torch.empty(cap, dtype=torch.uint8).pin_memory().numpy()
+    offs = torch.empty(hc.n + 1, dtype=torch.int64).pin_memory().numpy().view(np.uint64)
+    best = None
+    for chunk in (1 << 18, 1 << 20):
+        for _ in range(2):
+            t0 = time.perf_counter()
+            encode_host_batch(schema, hc, chunk_blobs=chunk, want_status=False, out=out, offsets=offs)
+            el = time.perf_counter() - t0
+            if best is None or el < best[0]:
+                best = (el, chunk)
+    el, chunk = best
+    tot = int(offs[hc.n])
+    return {"million_blobs_per_s": round(hc.n / el / 1e6, 3), "gib_per_s_out": round(tot / el / 2 ** 30, 3),
+            "gib_per_s_in_plus_out": round((tot + hc.nbytes_in()) / el / 2 ** 30, 3),
+            "chunk_blobs": chunk, "note": "pinned host columns -> packos_encode_host_batch -> pinned host arena"}
+
+
+# ----------------------------------------------------------------- main
 def main():
     args = parse()
     import torch
@@ -82,89 +167,108 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    from packos_amd.api import CompiledSchema, DeviceColumns, EncodePlan, encode_batch
-    from packos_amd.configs import CONFIGS, algorithmic_bytes, make_columns
+    from packos_amd.api import CompiledSchema, DeviceColumns, EncodePlan
+    from packos_amd.configs import CONFIGS, algorithmic_bytes, global_blob_sizes, make_columns
+    from packos_amd.shard import plan_shards
 
     cfg = CONFIGS[args.config]
-    n = args.n or (cfg.n // 8 if args.config == "C5" else cfg.n)
-    seed = cfg.seed + rank
-    hc = make_columns(cfg, n=n, seed=seed)
     schema = CompiledSchema(cfg.chain, cfg.mode)
-    dcols = DeviceColumns.from_host(schema, hc, dev)
     fixed = schema.fixed_blob_size > 0
+    per_gpu = args.n or cfg.shard
+    n_global = per_gpu * world
+    if fixed:
+        sizes = np.full(n_global, schema.fixed_blob_size, dtype=np.int64)
+    else:
+        sizes = global_blob_sizes(cfg, n_global, schema.all_present_size())
+    shards = plan_shards(sizes, world)
+    lo, hi = shards[rank]
+    del sizes
+    n = hi - lo
+    hc = make_columns(cfg, n=n, lo=lo)
     stream = torch.cuda.current_stream()
 
-    # output buffers allocated once; for fixed-size schemas blob i is at i*B
-    r = encode_batch(schema, dcols, want_offsets=not fixed, want_status=False)
+    # S device copies of the shard: distinct column buffers and output arenas
+    sets = []
+    base = DeviceColumns.from_host(schema, hc, dev)
+    for s in range(max(1, args.sets)):
+        if s == 0:
+            dc = base
+        else:
+            cl = lambda xs: [None if x is None else x.clone() for x in xs]  # noqa: E731
+            dc = DeviceColumns(schema, n, cl(base.data), cl(base.offsets), cl(base.valid))
+        sets.append(EncodePlan(schema, dc, stream=stream))
     torch.cuda.synchronize()
-    total_out = r.total
-    out = r.arena
+    total_out = sets[0].total
+    footprint = sum(p.cols.nbytes() + p.out.numel() for p in sets)
 
-    # one step = one plan replay: fixed -> one encode launch; var -> size kernel
-    # + encode kernel, all on `stream`, no host sync
-    plan = EncodePlan(schema, dcols, out=out, stream=stream)
-    step = plan.run
+    def timed(plans, steps, warmup):
+        for k in range(warmup):
+            plans[k % len(plans)].run()
+        torch.cuda.synchronize()
+        # HIP events on the launch stream bracket the timed region: elapsed / K
+        # is the average step duration on the GPU (a fixed schema's step is the
+        # one encode kernel; agrees with rocprofv3 --kernel-trace).
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for k in range(steps):
+            plans[k % len(plans)].run()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, ev0.elapsed_time(ev1) / steps
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    # HIP events on the launch stream bracket the timed region: elapsed / K is
-    # the average launch duration (a fixed schema's step is the one encode
-    # kernel; agrees with rocprofv3 --kernel-trace).  Per-step event pairs are
-    # not used: each timing event record costs ~9 us of GPU time here
-    # (tools/hostcost.py), i.e. they would perturb what they measure.
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    # this rank's time ends when its GPU work has drained; the trailing
-    # barrier keeps the ranks together and the MAX over ranks below reports
-    # the slowest one (a barrier inside the clock would add its own latency)
-    el = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    warm_el, warm_kms = (None, None) if args.no_warm else timed(sets[:1], args.steps, args.warmup)
+    el, kernel_ms = timed(sets, args.steps, args.warmup)
 
     alg = algorithmic_bytes(hc, total_out, with_offsets=not fixed)
-    blobs = n * args.steps * world
+    blobs = n_global * args.steps
     value = blobs / el / 1e6
     achieved = alg / (kernel_ms * 1e-3) / 1e9
+    warm_achieved = alg / (warm_kms * 1e-3) / 1e9 if warm_kms else None
 
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}.json")
+    # PMC traffic is not collected in this process (rocprofv3 --pmc runs are
+    # separate passes of this same command); the summary of such a pass, with
+    # its provenance, is read from profiles/ when present.
+    traffic, traffic_src = None, None
+    pmc_path = os.path.join(ROOT, "profiles", "r02", f"pmc_{args.config}.json")
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
                 pmc = json.load(f)
             traffic = pmc.get("hbm_bytes_per_launch")
+            traffic_src = f"profiles/r02/pmc_{args.config}.json: {pmc.get('source', '')}"
         except Exception:
             traffic = None
 
-    e2e = None
-    if args.e2e and rank == 0:
-        e2e = e2e_rate(schema, cfg, hc, dev, fixed)
-
-    cpu = None
+    cpu, parity, host = None, None, None
     if rank == 0 and world == 1 and not args.no_cpu:
-        nsamp = min(n, 1 << 20)
-        hs = make_columns(cfg, n=nsamp, seed=seed)
-        res = cpu_baseline(cfg, hs, args.cpu_seconds)
+        gpu_arena = sets[0].out[:total_out].cpu().numpy()
+        gpu_offs = None if fixed else sets[0].offsets.cpu().numpy()
+        res, hi_, same, digest, tot = cpu_leg(cfg, hc, args.cpu_seconds, gpu_arena, gpu_offs)
         mt = res["mt"]
         cpu = {"value": round(mt[0] / 1e6, 4), "unit": "million blobs/s", "cores": mt[3], "kind": "port",
-               "sample": f"{nsamp} blobs of config {args.config} (same generator, rank-0 seed), "
-                         f"{mt[1]} passes in {mt[2]:.1f} s; C restatement of PutAccess/Pack "
-                         f"(oracle/), {mt[3]} threads",
-               "single_thread_value": round(res['st'][0] / 1e6, 4)}
+               "sample": f"the whole shard ({n} blobs of config {args.config}), {mt[1]} passes in {mt[2]:.1f} s; "
+                         f"C restatement of PutAccess/Pack (oracle/), {mt[3]} threads = every CPU this "
+                         f"process may run on",
+               "single_thread_value": round(res['st'][0] / 1e6, 4),
+               "nproc": hi_["nproc"], "affinity": hi_["affinity"], "cgroup_cpu_quota": hi_["cgroup_cpu_quota"],
+               "cpu_model": hi_["cpu_model"]}
+        parity = {"result": "bit-exact" if same else "MISMATCH", "blobs": n, "bytes": tot,
+                  "sha256_16": digest, "checked": "GPU arena of the timed run vs the CPU oracle, whole shard"}
+    if rank == 0 and world == 1 and not args.no_host:
+        try:
+            host = host_leg(schema, make_columns(cfg, n=min(n, 1 << 22), lo=lo))
+        except Exception as e:  # reported, never fatal for the device-resident metric
+            host = {"error": str(e)[:200]}
 
     if rank == 0:
         line = {
@@ -179,65 +283,30 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (splitmix64, seed 0x%X + rank)" % cfg.seed,
-            "config": {"workload": f"{args.config}: {cfg.note}", "blobs_per_gpu": n,
+            "data": "synthetic (splitmix64 indexed by global blob, seed 0x%X)" % cfg.seed,
+            "config": {"workload": f"{args.config}: {cfg.note}", "blobs_per_gpu": n, "global_blobs": n_global,
                        "blob_bytes": schema.fixed_blob_size if fixed else round(total_out / n, 1),
-                       "parallelism": f"dp{world} (independent shards, no collective)"},
-            "gib_per_s": round(total_out * args.steps * world / el / 2 ** 30, 2),
+                       "parallelism": f"dp{world} (byte-balanced disjoint shards, no collective)",
+                       "sets_rotated": len(sets), "footprint_mib": round(footprint / 2 ** 20, 1)},
+            "gib_per_s": round(total_out * n_global / n * args.steps / el / 2 ** 30, 2),
             "kernel_ms": round(kernel_ms, 5),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
-                         "algorithmic_bytes_per_launch": alg},
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": alg,
+                         "cache_state": f"cold: {len(sets)} sets rotated ({footprint / 2 ** 20:.0f} MiB > 256 MiB "
+                                        "Infinity Cache)"},
+            "warm": None if warm_kms is None else {
+                "kernel_ms": round(warm_kms, 5), "achieved": round(warm_achieved, 1),
+                "frac": round(warm_achieved / HBM_PEAK_GBS, 4), "ms_per_step": round(warm_el / args.steps * 1e3, 4),
+                "note": "set 0 replayed back to back (inputs may stay in the Infinity Cache)"},
             "cpu_baseline": cpu,
+            "parity": parity,
+            "host_resident": host,
         }
-        if e2e is not None:
-            line["e2e_pinned"] = e2e
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
-
-
-def e2e_rate(schema, cfg, hc, dev, fixed):
-    """Pinned host columns -> H2D -> encode -> D2H into pinned memory, chunked
-    and double-buffered on two streams (recorded in DESIGN.md, never `value`)."""
-    import torch
-    from packos_amd.api import DeviceColumns, encode_batch
-    n = hc.n
-    chunk = max(1, n // 8)
-    B = schema.fixed_blob_size
-    if not fixed:
-        return None
-    pin_cols = []
-    for c, sp in enumerate(schema.specs):
-        d = hc.data[c]
-        pin_cols.append(torch.from_numpy(d).pin_memory() if d is not None else None)
-    out_host = torch.empty(n * B, dtype=torch.uint8).pin_memory()
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-    bufs = []
-    for k in range(2):
-        cols = [None if p is None else torch.empty(chunk * sp.width, dtype=torch.uint8, device=dev)
-                for p, sp in zip(pin_cols, schema.specs)]
-        bufs.append((cols, torch.empty(chunk * B, dtype=torch.uint8, device=dev)))
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for j, s0 in enumerate(range(0, n, chunk)):
-        k = j % 2
-        m = min(chunk, n - s0)
-        st = streams[k]
-        cols, out = bufs[k]
-        with torch.cuda.stream(st):
-            for c, sp in enumerate(schema.specs):
-                if pin_cols[c] is not None:
-                    cols[c][: m * sp.width].copy_(pin_cols[c][s0 * sp.width:(s0 + m) * sp.width],
-                                                 non_blocking=True)
-            dc = DeviceColumns(schema, m, cols, [None] * len(cols), [None] * len(cols))
-            encode_batch(schema, dc, want_offsets=False, want_status=False, out=out, stream=st)
-            out_host[s0 * B:(s0 + m) * B].copy_(out[: m * B], non_blocking=True)
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    return {"million_blobs_per_s": round(n / el / 1e6, 3), "gib_per_s_out": round(n * B / el / 2 ** 30, 3),
-            "chunks": (n + chunk - 1) // chunk, "note": "pinned H2D + encode + D2H, 2 streams"}
 
 
 if __name__ == "__main__":

@@ -340,6 +340,9 @@ int64_t or_encode_one(const or_schema* s, const packos_column* cols, size_t i, i
     return r;
 }
 
+/* batch calls use up to this many threads (every core of a large host) */
+#define OR_MAX_THREADS 1024
+
 typedef struct enc_job {
     const or_schema* s; const packos_column* cols; int mode;
     uint8_t* out; uint64_t* offs; uint32_t* status; size_t lo, hi;
@@ -371,9 +374,10 @@ static void* size_worker(void* arg) {
 int64_t or_encode_batch(const or_schema* s, const packos_column* cols, size_t n, int mode, uint8_t* out,
                         size_t cap, uint64_t* out_offsets, uint32_t* status, int nthreads) {
     if (nthreads < 1) nthreads = 1;
-    if (nthreads > 256) nthreads = 256;
-    pthread_t th[256];
-    size_job sj[256];
+    if (nthreads > OR_MAX_THREADS) nthreads = OR_MAX_THREADS;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+    size_job* sj = (size_job*)malloc(sizeof(size_job) * (size_t)nthreads);
+    enc_job* ej = (enc_job*)malloc(sizeof(enc_job) * (size_t)nthreads);
     size_t per = (n + (size_t)nthreads - 1) / (size_t)nthreads;
     out_offsets[0] = 0;
     for (int t = 0; t < nthreads; t++) {
@@ -384,8 +388,7 @@ int64_t or_encode_batch(const or_schema* s, const packos_column* cols, size_t n,
     }
     for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
     for (size_t i = 0; i < n; i++) out_offsets[i + 1] += out_offsets[i];
-    if (out_offsets[n] > cap) return -1;
-    enc_job ej[256];
+    if (out_offsets[n] > cap) { free(th); free(sj); free(ej); return -1; }
     for (int t = 0; t < nthreads; t++) {
         size_t lo = (size_t)t * per, hi = lo + per > n ? n : lo + per;
         if (lo > hi) lo = hi;
@@ -393,6 +396,7 @@ int64_t or_encode_batch(const or_schema* s, const packos_column* cols, size_t n,
         pthread_create(&th[t], NULL, enc_worker, &ej[t]);
     }
     for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    free(th); free(sj); free(ej);
     return (int64_t)out_offsets[n];
 }
 
@@ -582,9 +586,9 @@ static void* dec_worker(void* arg) {
 int or_decode_batch(const or_schema* s, const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
                     size_t n, packos_column* cols, uint32_t* status, int nthreads) {
     if (nthreads < 1) nthreads = 1;
-    if (nthreads > 256) nthreads = 256;
-    pthread_t th[256];
-    dec_job dj[256];
+    if (nthreads > OR_MAX_THREADS) nthreads = OR_MAX_THREADS;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+    dec_job* dj = (dec_job*)malloc(sizeof(dec_job) * (size_t)nthreads);
     size_t per = (n + (size_t)nthreads - 1) / (size_t)nthreads;
     for (int t = 0; t < nthreads; t++) {
         size_t lo = (size_t)t * per, hi = lo + per > n ? n : lo + per;
@@ -593,6 +597,7 @@ int or_decode_batch(const or_schema* s, const uint8_t* arena, const uint64_t* of
         pthread_create(&th[t], NULL, dec_worker, &dj[t]);
     }
     for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    free(th); free(dj);
     return 0;
 }
 

@@ -22,10 +22,11 @@ from .schema import (SBool, SBytes, SFloat64, SInt16, SInt32, SInt64, SMapSorted
 GOLDEN_GAMMA = np.uint64(0x9E3779B97F4A7C15)
 
 
-def splitmix64(seed: int, count: int) -> np.ndarray:
-    """splitmix64 outputs z_1..z_count for state `seed` (state += gamma first)."""
+def splitmix64(seed: int, count: int, start: int = 0) -> np.ndarray:
+    """splitmix64 outputs z_{start+1}..z_{start+count} for state `seed`
+    (counter-based: any slice of the stream is generated directly)."""
     with np.errstate(over="ignore"):
-        k = np.arange(1, count + 1, dtype=np.uint64)
+        k = np.arange(start + 1, start + count + 1, dtype=np.uint64)
         z = np.uint64(seed) + k * GOLDEN_GAMMA
         z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
@@ -33,9 +34,21 @@ def splitmix64(seed: int, count: int) -> np.ndarray:
     return z
 
 
-def random_bytes(seed: int, nbytes: int) -> np.ndarray:
-    words = splitmix64(seed, (nbytes + 7) // 8)
-    return words.view(np.uint8)[:nbytes].copy()
+def random_bytes(seed: int, nbytes: int, byte_off: int = 0) -> np.ndarray:
+    """Bytes [byte_off, byte_off + nbytes) of the little-endian splitmix64
+    byte stream of `seed`; generated in bounded pieces (large shards)."""
+    out = np.empty(nbytes, dtype=np.uint8)
+    piece = 1 << 28
+    done = 0
+    while done < nbytes:
+        m = min(piece, nbytes - done)
+        b0 = byte_off + done
+        w0 = b0 // 8
+        w1 = (b0 + m + 7) // 8
+        words = splitmix64(seed, w1 - w0, start=w0)
+        out[done:done + m] = words.view(np.uint8)[b0 - 8 * w0: b0 - 8 * w0 + m]
+        done += m
+    return out
 
 
 def _col_seed(seed: int, c: int) -> int:
@@ -49,19 +62,27 @@ class Config:
     n: int
     seed: int
     mode: int = 0
-    var_len: Optional[Callable] = None   # (n, seed) -> dict col -> lengths
+    var_len: Optional[Callable] = None   # (n, seed, lo) -> dict col -> lengths of blobs [lo, lo + n)
     note: str = ""
+    per_gpu: int = 0                     # blobs one GPU encodes in bench.py (0: n)
+
+    @property
+    def shard(self) -> int:
+        return self.per_gpu or self.n
 
 
-def fixed_columns(chain: SchemaChain, n: int, seed: int, var_lengths: Optional[Dict[int, np.ndarray]] = None
-                  ) -> HostColumns:
-    """Synthetic HostColumns for any schema (no nils)."""
+def fixed_columns(chain: SchemaChain, n: int, seed: int, var_lengths: Optional[Dict[int, np.ndarray]] = None,
+                  lo: int = 0, var_base: Optional[Dict[int, int]] = None) -> HostColumns:
+    """Synthetic HostColumns (no nils) for blobs [lo, lo + n) of the global
+    batch of `seed`: row i of every column depends only on the global blob
+    index, so the shards of a batch concatenate to the unsharded batch.
+    `var_base[c]` = arena bytes of var column c before blob lo."""
     hc = HostColumns(chain, n)
     for c, sp in enumerate(hc.specs):
         node = sp.node
         s = _col_seed(seed, c)
         if sp.fixed:
-            raw = random_bytes(s, n * sp.width)
+            raw = random_bytes(s, n * sp.width, byte_off=lo * sp.width)
             if node.kind == "bool":
                 raw &= 1
             elif node.kind == "string":
@@ -74,9 +95,11 @@ def fixed_columns(chain: SchemaChain, n: int, seed: int, var_lengths: Optional[D
             np.cumsum(lens, out=offs[1:])
             if offs[-1] >= 2 ** 32:
                 raise ValueError("var column arena exceeds uint32 offsets; shard the batch")
-            raw = random_bytes(s, int(offs[-1]))
+            base = int(var_base.get(c, 0)) if var_base else 0
+            raw = random_bytes(s, int(offs[-1]), byte_off=base)
             if node.kind == "string":
-                raw = (0x20 + (raw % 95)).astype(np.uint8)
+                np.remainder(raw, 95, out=raw)
+                raw += 0x20
             hc.data[c] = raw
             hc.offsets[c] = offs.astype(np.uint32)
         elif sp.has_valid:
@@ -102,14 +125,14 @@ CHAIN_C4 = SChain(SInt16, SInt64, SBool, SStringLen(103),
 CHAIN_C5 = SChain(SInt16, SInt64, SBool, SVariableString(), SVariableBytes())
 
 
-def c3_lengths(n: int, seed: int) -> Dict[int, np.ndarray]:
-    r = splitmix64(seed ^ 0xC3C3, n)
+def c3_lengths(n: int, seed: int, lo: int = 0) -> Dict[int, np.ndarray]:
+    r = splitmix64(seed ^ 0xC3C3, n, start=lo)
     return {4: (8 + (r % np.uint64(33))).astype(np.uint32)}  # column 4 = SString, 8..40 B
 
 
-def c5_lengths(n: int, seed: int) -> Dict[int, np.ndarray]:
+def c5_lengths(n: int, seed: int, lo: int = 0) -> Dict[int, np.ndarray]:
     """Blob size log-uniform in [64, 4096]: B = 12 (H) + 11 + ls + lb."""
-    r = splitmix64(seed ^ 0xC5C5, n).astype(np.float64) / 2.0 ** 64
+    r = splitmix64(seed ^ 0xC5C5, n, start=lo).astype(np.float64) / 2.0 ** 64
     B = np.floor(np.exp(np.log(64.0) + r * (np.log(4096.0) - np.log(64.0)))).astype(np.int64)
     B = np.clip(B, 64, 4096)
     rest = B - 23
@@ -126,16 +149,41 @@ CONFIGS = {
     "C3": Config("C3", CHAIN_C3, 1 << 20, 0x5EED0003, var_len=c3_lengths,
                  note="1M schema-guided records, encode+decode"),
     "C4": Config("C4", CHAIN_C4, 4 << 20, 0x5EED0004, note="4M x 256 B with nested PackMapSorted"),
-    "C5": Config("C5", CHAIN_C5, 64 << 20, 0x5EED0005, var_len=c5_lengths,
-                 note="64M mixed 64 B-4 KB across 8 GPUs (per-shard seed + shard)"),
+    "C5": Config("C5", CHAIN_C5, 64 << 20, 0x5EED0005, var_len=c5_lengths, per_gpu=(64 << 20) // 8,
+                 note="64M mixed 64 B-4 KB across 8 GPUs (one GPU = one 8,388,608-blob shard)"),
 }
 
 
-def make_columns(cfg: Config, n: Optional[int] = None, seed: Optional[int] = None) -> HostColumns:
+def var_prefix(cfg: Config, lo: int, seed: Optional[int] = None) -> Dict[int, int]:
+    """Arena bytes of every var column before global blob `lo`."""
+    seed = cfg.seed if seed is None else seed
+    base: Dict[int, int] = {}
+    if not cfg.var_len or lo == 0:
+        return base
+    step = 1 << 22
+    for a in range(0, lo, step):
+        for c, l in cfg.var_len(min(step, lo - a), seed, a).items():
+            base[c] = base.get(c, 0) + int(np.asarray(l, dtype=np.uint64).sum())
+    return base
+
+
+def make_columns(cfg: Config, n: Optional[int] = None, seed: Optional[int] = None, lo: int = 0) -> HostColumns:
+    """Blobs [lo, lo + n) of config `cfg`'s synthetic batch."""
     n = cfg.n if n is None else n
     seed = cfg.seed if seed is None else seed
-    vl = cfg.var_len(n, seed) if cfg.var_len else None
-    return fixed_columns(cfg.chain, n, seed, vl)
+    vl = cfg.var_len(n, seed, lo) if cfg.var_len else None
+    return fixed_columns(cfg.chain, n, seed, vl, lo=lo, var_base=var_prefix(cfg, lo, seed))
+
+
+def global_blob_sizes(cfg: Config, n_global: int, static_size: int, seed: Optional[int] = None) -> np.ndarray:
+    """Encoded size of every blob of a global batch of the config (no nils:
+    the schema's static bytes + the var lengths), for shard planning."""
+    seed = cfg.seed if seed is None else seed
+    sizes = np.full(n_global, static_size, dtype=np.int64)
+    if cfg.var_len:
+        for c, l in cfg.var_len(n_global, seed, 0).items():
+            sizes += np.asarray(l, dtype=np.int64)
+    return sizes
 
 
 def algorithmic_bytes(hc: HostColumns, total_out: int, with_offsets: bool) -> int:
