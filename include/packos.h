@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define PACKOS_ABI_VERSION 1
+#define PACKOS_ABI_VERSION 2
 
 /* ---- return codes (library-level errors) -------------------------------- */
 #define PACKOS_OK              0
@@ -114,7 +114,10 @@ extern "C" {
  *   fixed-width leaf : data = n*width bytes, row i at data + i*width
  *                      (16-byte aligned base; little-endian scalars)
  *   var-width leaf   : encode input: data = byte arena, offsets = n+1 uint32
- *                      (row i = data[offsets[i] .. offsets[i+1]))
+ *                      (row i = data[offsets[i] .. offsets[i+1])); or
+ *                      offsets64 = n+1 uint64 for arenas past 4 GiB (when
+ *                      offsets64 is set it is used and offsets is ignored;
+ *                      one value must stay below 4 GiB)
  *                      decode output: start[i] = absolute arena offset of the
  *                      payload, length[i] = its width (the payload aliases the
  *                      input arena, like GetBytes/GetStringUnsafe,
@@ -129,6 +132,7 @@ typedef struct packos_column {
     uint8_t*        valid;
     uint64_t*       start;
     uint32_t*       length;
+    const uint64_t* offsets64;   /* ABI 2: 64-bit var offsets (encode input), NULL = use offsets */
 } packos_column;
 
 typedef struct packos_column_info {
@@ -178,12 +182,11 @@ int64_t packos_schema_blob_size_host(const packos_schema* s, const uint32_t* wid
 
 /* ---- batch encode ---------------------------------------------------------- */
 
-/* Device scratch a variable-size batch of n blobs needs: scan tile sums
- * (size pass), per-tile flags and per-blob value positions of the tiled
- * variable-size encoder.  packos_encoded_size_batch requires it;
- * packos_encode_batch uses it when given (without it, a variable-size batch
- * with PACKOS_ENC_OFFSETS_READY runs the slower one-wavefront-per-blob
- * kernel).  Fixed-size batches need none. */
+/* Device scratch a variable-size batch of n blobs may need: the look-back
+ * words of the size pass when blob sizes depend on nil values.  Batches whose
+ * presence is data-independent (no nil container / nullable value in the
+ * call) need none: their out_offsets have a closed form.  Fixed-size batches
+ * need none. */
 size_t packos_encode_workspace_size(const packos_schema* s, size_t n_blobs);
 
 /* Size pass + exclusive scan: out_offsets[0..n] (device, uint64).  Fixed-size
@@ -193,9 +196,10 @@ int packos_encoded_size_batch(const packos_schema* s, const packos_column* cols,
                               void* stream);
 
 /* Encode n blobs into out_arena.  For a variable-size schema out_offsets
- * (n+1, device) receives each blob's start; pass flags PACKOS_ENC_OFFSETS_READY
- * when out_offsets already holds the result of packos_encoded_size_batch to
- * skip the size pass.  For a fixed-size schema out_offsets may be NULL (blob i
+ * (n+1, device) receives each blob's start (computed in the encode kernel
+ * itself when no presence depends on the data, else by a size pass first);
+ * pass flags PACKOS_ENC_OFFSETS_READY when out_offsets already holds the
+ * layout to encode into (e.g. from packos_encoded_size_batch).  For a fixed-size schema out_offsets may be NULL (blob i
  * is at i*B).  status (n, device) may be NULL.  out_capacity is checked only
  * when offsets are known on the host side (fixed schemas); for variable
  * schemas blobs that would end past out_capacity are not written and get
@@ -207,14 +211,14 @@ int packos_encoded_size_batch(const packos_schema* s, const packos_column* cols,
 #define PACKOS_ENC_OFFSETS_READY 1u
 /* testing/benchmark knob: fixed-size batches use the general 4-blob-period
  * kernel even when the lane-invariant one applies; variable-size batches use
- * the one-wavefront-per-blob kernel instead of the tiled one                 */
+ * the generic one-wavefront-per-blob kernel instead of the tiled one         */
 #define PACKOS_ENC_FORCE_GENERIC 2u
 /* testing/benchmark knob: pick the fixed-layout kernel variant (0 = auto):
  * 13 one tile per workgroup, LDS-DMA staging, single-source dwords (auto
  *    when B % 4 == 0, 16 <= B <= 1024, <= 16 fixed columns);
- * 1, 2 lane-invariant dword kernel {plain, NT stores} (auto otherwise when
- *    B % 4 == 0; also the partial last tile of variant 13);
- * 8 general 4-blob-period kernel (any B)                                     */
+ * 2  lane-invariant dword kernel (auto otherwise when B % 4 == 0; also the
+ *    partial last tile of variant 13);
+ * 8  general 4-blob-period kernel (any B)                                    */
 #define PACKOS_ENC_FIXED_VARIANT(v) (((uint32_t)(v) & 0xFu) << 4)
 int packos_encode_batch(const packos_schema* s, const packos_column* cols, size_t n_blobs,
                         uint8_t* out_arena, uint64_t out_capacity, uint64_t* out_offsets,
@@ -266,6 +270,38 @@ int packos_get_field_batch(const uint8_t* arena, const uint64_t* offsets, uint64
                            size_t n_blobs, const int32_t* path, int depth, int want_tag,
                            int want_width, uint64_t* out_start, uint32_t* out_len,
                            uint8_t* out_tag, uint8_t* status, void* stream);
+
+/* General GetAccess getter over every blob (walk `depth` positions like
+ * packos_get_field_batch, then apply one Get* family to the last position):
+ *   PACKOS_GET_FIXED     Get{Bool,Int8..64,Uint8..64,Float32/64}: tag ==
+ *                        want_tag and width == want_width (access/get.go:60-66,
+ *                        :80-94, :173-226, :287-305)
+ *   PACKOS_GET_NULLABLE  GetNullable*: width 0 -> status 4 (nil, no error),
+ *                        checked BEFORE the tag; otherwise as FIXED
+ *                        (access/get.go:68-78, :96-118, :214-284, :307-333)
+ *   PACKOS_GET_SPAN      GetBytes / GetString(Unsafe): tag == want_tag and
+ *                        end >= start (access/get.go:335-375)
+ *   PACKOS_GET_INT       GetInt: tag Integer (checked first), width 0 -> nil,
+ *                        1/2/4/8 -> int8..int64 (access/get.go:120-146)
+ *   PACKOS_GET_FLOAT     GetFloating: tag Floating, width 0 -> nil, 4/8
+ *                        (access/get.go:148-170)
+ * Typed gather: when out_values is not NULL, row i of out_values
+ * (value_width bytes) receives the value of a successful FIXED / NULLABLE
+ * getter (its LE bytes; a Bool as 0/1), or for INT the integer sign-extended
+ * to int64, for FLOAT the raw bits (a float32 in the low 4 bytes); zero
+ * otherwise.  value_width: want_width for FIXED / NULLABLE, 8 for INT / FLOAT.
+ * status: 0 ok, 1 decode error, 2 nil nested accessor (empty container on
+ * the path), 3 nil accessor (NewGetAccess would return nil: the reference
+ * panics), 4 nil value.                                                      */
+#define PACKOS_GET_FIXED     0
+#define PACKOS_GET_NULLABLE  1
+#define PACKOS_GET_SPAN      2
+#define PACKOS_GET_INT       3
+#define PACKOS_GET_FLOAT     4
+int packos_get_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride, size_t n_blobs,
+                     const int32_t* path, int depth, int getter, int want_tag, int want_width,
+                     uint8_t* out_values, uint32_t value_width, uint64_t* out_start, uint32_t* out_len,
+                     uint8_t* out_tag, uint8_t* status, void* stream);
 
 /* ---- misc ------------------------------------------------------------------ */
 const char* packos_strerror(int code);

@@ -684,6 +684,90 @@ int or_get_field_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t s
     return 0;
 }
 
+/* packos_get_batch contract (include/packos.h).  Each getter restates the
+ * matching Get* family of access/get.go:
+ *   FIXED     Get{Bool,Int8..64,Uint8..64,Float32/64}: tag and exact width
+ *             (get.go:60-66, 80-94, 173-226, 287-305); value = the LE bytes,
+ *             a Bool normalised to 0/1 (g.buf[start] != 0)
+ *   NULLABLE  GetNullable*: width 0 -> (nil, nil) BEFORE the tag check
+ *             (get.go:68-78, 96-118, 214-284, 307-333)
+ *   SPAN      GetBytes / GetString(Unsafe): tag and end >= start (get.go:335-375)
+ *   INT       GetInt: tag Integer first, then width 0 -> nil, 1/2/4/8 ->
+ *             int8..int64 (sign-extended to 8 bytes), else error (get.go:120-146)
+ *   FLOAT     GetFloating: tag Floating first, then 0 -> nil, 4/8 -> raw bits
+ *             (8-byte slot, float32 bits low), else error (get.go:148-170)
+ * status: 0 ok, 1 decode error, 2 nil nested accessor, 3 nil accessor (the
+ * reference dereferences nil: panic), 4 nil value (no error). */
+int or_get_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride, size_t n,
+                 const int32_t* path, int depth, int getter, int want_tag, int want_width,
+                 uint8_t* out_values, uint32_t value_width, uint64_t* out_start, uint32_t* out_len,
+                 uint8_t* out_tag, uint8_t* status) {
+    for (size_t i = 0; i < n; i++) {
+        uint64_t a = offsets ? offsets[i] : i * stride;
+        uint64_t b = offsets ? offsets[i + 1] : (i + 1) * stride;
+        or_get g;
+        out_start[i] = 0; out_len[i] = 0; out_tag[i] = 0;
+        if (out_values) memset(out_values + i * value_width, 0, value_width);
+        if (!or_get_init(&g, arena + a, (int64_t)(b - a))) { status[i] = 3; continue; }
+        uint64_t base = a;
+        int st = 0;
+        for (int d = 0; d < depth - 1 && !st; d++) {
+            or_get nx; int tp;
+            int r = or_get_nested(&g, path[d], &nx, &tp);
+            if (r) { st = r; break; }
+            base += (uint64_t)(nx.buf - g.buf);
+            g = nx;
+        }
+        if (st) { status[i] = (uint8_t)st; continue; }
+        int tp; int64_t s0, e0;
+        or_get_range(&g, path[depth - 1], &tp, &s0, &e0);
+        out_tag[i] = (uint8_t)tp;
+        const int64_t w = e0 - s0;
+        int r = 0;
+        switch (getter) {
+            case PACKOS_GET_NULLABLE:
+                if (w == 0) { r = 4; break; }
+                /* fall through */
+            case PACKOS_GET_FIXED:
+                if (tp != want_tag || w != want_width) r = 1;
+                break;
+            case PACKOS_GET_SPAN:
+                if (tp != want_tag || e0 < s0) r = 1;
+                break;
+            case PACKOS_GET_INT:
+                if (tp != PACKOS_TAG_INTEGER) r = 1;
+                else if (w == 0) r = 4;
+                else if (w != 1 && w != 2 && w != 4 && w != 8) r = 1;
+                break;
+            case PACKOS_GET_FLOAT:
+                if (tp != PACKOS_TAG_FLOATING) r = 1;
+                else if (w == 0) r = 4;
+                else if (w != 4 && w != 8) r = 1;
+                break;
+            default:
+                r = 1;
+        }
+        status[i] = (uint8_t)r;
+        if (r) continue;
+        out_start[i] = base + (uint64_t)s0;
+        out_len[i] = (uint32_t)w;
+        if (!out_values || getter == PACKOS_GET_SPAN) continue;
+        const uint8_t* src = g.buf + s0;
+        uint8_t* dst = out_values + i * value_width;
+        if (getter == PACKOS_GET_INT) {
+            uint64_t v = 0;
+            for (int k = 0; k < w; k++) v |= (uint64_t)src[k] << (8 * k);
+            if (w < 8 && (v >> (8 * w - 1)) & 1) v |= ~0ull << (8 * w);   /* int8..int32 -> int64 */
+            for (int k = 0; k < 8 && k < (int)value_width; k++) dst[k] = (uint8_t)(v >> (8 * k));
+        } else if (tp == PACKOS_TAG_BOOL && w == 1) {
+            dst[0] = src[0] != 0;
+        } else {
+            for (int64_t k = 0; k < w && k < (int64_t)value_width; k++) dst[k] = src[k];
+        }
+    }
+    return 0;
+}
+
 uint64_t or_splitmix64(uint64_t* state) {
     uint64_t z = (*state += 0x9E3779B97F4A7C15ull);
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

@@ -34,13 +34,13 @@ EXPORTED = [
     "packos_schema_decode_fast",
     "packos_schema_describe", "packos_schema_blob_size_host", "packos_encode_workspace_size",
     "packos_encoded_size_batch", "packos_encode_batch", "packos_encode_host_batch", "packos_decode_batch",
-    "packos_get_field_batch", "packos_strerror", "packos_last_error", "packos_abi_version",
+    "packos_get_field_batch", "packos_get_batch", "packos_strerror", "packos_last_error", "packos_abi_version",
 ]
 
 
 class PackosColumn(C.Structure):
     _fields_ = [("data", C.c_void_p), ("offsets", C.c_void_p), ("valid", C.c_void_p),
-                ("start", C.c_void_p), ("length", C.c_void_p)]
+                ("start", C.c_void_p), ("length", C.c_void_p), ("offsets64", C.c_void_p)]
 
 
 class PackosColumnInfo(C.Structure):
@@ -94,6 +94,8 @@ def lib():
     L.packos_decode_batch.argtypes = [vp, vp, vp, u64, sz, C.POINTER(PackosColumn), vp, vp]
     L.packos_get_field_batch.argtypes = [vp, vp, u64, sz, C.POINTER(C.c_int32), i32, i32, i32,
                                          vp, vp, vp, vp, vp]
+    L.packos_get_batch.argtypes = [vp, vp, u64, sz, C.POINTER(C.c_int32), i32, i32, i32, i32,
+                                   vp, u32, vp, vp, vp, vp, vp]
     L.packos_strerror.argtypes = [i32]
     L.packos_strerror.restype = C.c_char_p
     L.packos_last_error.restype = C.c_char_p

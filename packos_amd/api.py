@@ -27,7 +27,8 @@ from .columns import HostColumns, column_specs
 from .schema import SchemaChain
 
 __all__ = ["CompiledSchema", "DeviceColumns", "DecodedColumns", "encode_batch", "decode_batch",
-           "get_field_batch", "MODE_PUTACCESS", "MODE_PACKABLE"]
+           "get_field_batch", "get_batch", "GET_FIXED", "GET_NULLABLE", "GET_SPAN", "GET_INT",
+           "GET_FLOAT", "MODE_PUTACCESS", "MODE_PACKABLE"]
 
 
 def _torch():
@@ -371,3 +372,36 @@ def get_field_batch(arena, offsets, n: int, path, want_tag: int, want_width: int
                                        ln.data_ptr(), tg.data_ptr(), st.data_ptr(), _stream_ptr(stream)),
           "packos_get_field_batch")
     return s0[:n], ln[:n], tg[:n], st[:n]
+
+
+# getter families of packos_get_batch (include/packos.h)
+GET_FIXED, GET_NULLABLE, GET_SPAN, GET_INT, GET_FLOAT = range(5)
+
+
+def get_batch(arena, offsets, n: int, path, getter: int, want_tag: int = 0, want_width: int = 0,
+              stride: int = 0, values: bool = True, stream=None):
+    """One GetAccess getter over every blob (access/get.go:60-375):
+    (values, start, length, tag, status).
+
+    `getter` picks the Get* family: GET_FIXED (Get{Bool,IntN,UintN,FloatN}),
+    GET_NULLABLE (GetNullable*: width 0 -> status 4 before the tag check),
+    GET_SPAN (GetBytes/GetString), GET_INT (GetInt: any of 1/2/4/8 bytes,
+    sign-extended to int64), GET_FLOAT (GetFloating: 4/8 bytes, raw bits).
+    `values` is an (n, value_width) uint8 tensor of the gathered typed values
+    (None for GET_SPAN or values=False); view it with .view(torch.int64) etc."""
+    torch = _torch()
+    dev = arena.device
+    vw = 8 if getter in (GET_INT, GET_FLOAT) else max(want_width, 0)
+    gather = values and getter != GET_SPAN and vw > 0
+    vals = torch.empty((max(n, 1), vw), dtype=torch.uint8, device=dev) if gather else None
+    s0 = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    ln = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    tg = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    st = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    p = (C.c_int32 * len(path))(*path)
+    check(lib().packos_get_batch(arena.data_ptr(), None if offsets is None else offsets.data_ptr(), stride, n,
+                                 p, len(path), getter, want_tag, want_width,
+                                 None if vals is None else vals.data_ptr(), vw if gather else 0,
+                                 s0.data_ptr(), ln.data_ptr(), tg.data_ptr(), st.data_ptr(), _stream_ptr(stream)),
+          "packos_get_batch")
+    return (None if vals is None else vals[:n]), s0[:n], ln[:n], tg[:n], st[:n]

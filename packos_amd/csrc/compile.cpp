@@ -376,7 +376,7 @@ struct Builder {
         // tile size: T blobs (multiple of 16 so tile in/out are whole 16-B chunks)
         // ~16 KiB of output per tile (env PACKOS_TILE_BYTES overrides, tuning only)
         int64_t tile_bytes = 16384;
-        if (const char* e = getenv("PACKOS_TILE_BYTES"))
+        if (const char* e = getenv("PACKOS_TILE_BYTES"))   // read once, at compile
             tile_bytes = std::min<int64_t>(16384, std::max<int64_t>(1024, atoll(e)));  // staging plan holds <= 16 KiB
         int T = (int)((tile_bytes / B) / 16 * 16);
         if (T < 16) T = 16;
@@ -426,7 +426,6 @@ struct Builder {
             }
         }
         s->dfix.clear();
-        uint32_t units = 0;
         for (const FixCol& fc : s->fcols) {
             DecFix df{};
             df.col = fc.col;
@@ -437,11 +436,8 @@ struct Builder {
             if (df.blob_off == UINT32_MAX) fail(PACKOS_E_SCHEMA, "internal: fixed column not in layout");
             df.flags = bm[df.blob_off].is_bool ? 1u : 0u;
             df.magic = fc.width > 1 ? (uint32_t)(((1ull << 32) + fc.width - 1) / fc.width) : 0u;
-            df.unit_begin = units;
-            units += (uint32_t)T * fc.width / 16;
             s->dfix.push_back(df);
         }
-        s->dfix_units = (int)units;
         if (s->fix_lds > 60 * 1024) return;
         // segments for each dword r of a 4-blob period
         s->fsegs.clear();
@@ -650,6 +646,13 @@ struct Builder {
 
 namespace packos {
 void set_error(const std::string& m) { g_err = m; }
+
+void read_tune(Tune& t) {
+    if (const char* e = getenv("PACKOS_VAR_PER")) t.var_per = std::max(0, std::min(256, atoi(e)));
+    t.sizes_scan = getenv("PACKOS_SIZES_SCAN") != nullptr;
+    t.decode_generic = getenv("PACKOS_DECODE_GENERIC") != nullptr;
+    if (const char* e = getenv("PACKOS_DEC_TILE_BYTES")) t.dec_tile_bytes = std::min(49152, std::max(1024, atoi(e)));
+}
 }  // namespace packos
 
 extern "C" {
@@ -712,6 +715,7 @@ int packos_schema_compile(const char* schema_json, int mode, packos_schema** out
         s->n_top = (int)list->arr.size();
         b.assign_columns(root);
         if ((int)s->col_node.size() > kMaxCols) fail(PACKOS_E_UNSUPPORTED, "more than 64 columns");
+        read_tune(s->tune);
         b.build_encode();
         b.build_fixed();
         b.build_decode();

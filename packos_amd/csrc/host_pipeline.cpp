@@ -87,7 +87,10 @@ extern "C" int packos_encode_host_batch(const packos_schema* cs, const packos_co
         kind[c].var = str && nd.width <= 0;
         kind[c].width = kind[c].fixed ? (uint32_t)nd.width : 0u;
         if ((kind[c].fixed || kind[c].var) && !hc[c].data) { set_error("host column without data"); return PACKOS_E_INVALID; }
-        if (kind[c].var && !hc[c].offsets) { set_error("host var column without offsets"); return PACKOS_E_INVALID; }
+        if (kind[c].var && !hc[c].offsets && !hc[c].offsets64) {
+            set_error("host var column without offsets");
+            return PACKOS_E_INVALID;
+        }
         any_valid |= hc[c].valid != nullptr;
     }
     const bool fixed_size = !s->has_var && !any_valid && s->all_present_size >= 0;
@@ -98,6 +101,12 @@ extern "C" int packos_encode_host_batch(const packos_schema* cs, const packos_co
     for (const EncItem& it : s->items)
         if (it.type != IT_VAR) stat += it.size;
 
+    // host var offsets of either width; every chunk's device offsets are
+    // chunk-relative uint32 (a chunk's var bytes must stay below 4 GiB), so
+    // 64-bit host offsets lift the 4 GiB limit of the whole batch
+    auto hoff = [&](size_t c, size_t i) -> uint64_t {
+        return hc[c].offsets64 ? hc[c].offsets64[i] : (uint64_t)hc[c].offsets[i];
+    };
     size_t chunk = chunk_blobs ? chunk_blobs : (size_t)1 << 20;
     chunk = std::min(chunk, n);
     const size_t nch = (n + chunk - 1) / chunk;
@@ -109,12 +118,17 @@ extern "C" int packos_encode_host_batch(const packos_schema* cs, const packos_co
         uint64_t vb = 0;
         for (size_t c = 0; c < ncol; c++)
             if (kind[c].var) {
-                const uint64_t b = (uint64_t)hc[c].offsets[s0 + m] - hc[c].offsets[s0];
+                const uint64_t b = hoff(c, s0 + m) - hoff(c, s0);
                 var_max[c] = std::max(var_max[c], b);
                 vb += b;
             }
         out_max = std::max(out_max, (uint64_t)m * stat + vb);
     }
+    for (size_t c = 0; c < ncol; c++)
+        if (var_max[c] >= (1ull << 32)) {
+            set_error("packos_encode_host_batch: a chunk's var bytes exceed 4 GiB (use smaller chunk_blobs)");
+            return PACKOS_E_INVALID;
+        }
 
     int dev = 0;
     HP_TRY(hipGetDevice(&dev));
@@ -183,12 +197,11 @@ extern "C" int packos_encode_host_batch(const packos_schema* cs, const packos_co
                 dc[c].data = sl.dfix[c];
             }
             if (kind[c].var) {
-                const uint32_t* o = hc[c].offsets;
-                const uint32_t o0 = o[s0];
-                for (size_t x = 0; x <= m; x++) sl.hoff[c][x] = o[s0 + x] - o0;   // chunk-relative offsets
+                const uint64_t o0 = hoff(c, s0);
+                for (size_t x = 0; x <= m; x++) sl.hoff[c][x] = (uint32_t)(hoff(c, s0 + x) - o0);   // chunk-relative
                 HP_TRY(hipMemcpyAsync(sl.doff[c], sl.hoff[c], (m + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
                                       sl.st));
-                const uint64_t vb = (uint64_t)o[s0 + m] - o0;
+                const uint64_t vb = hoff(c, s0 + m) - o0;
                 if (vb)
                     HP_TRY(hipMemcpyAsync(sl.dvar[c], (const uint8_t*)hc[c].data + o0, vb, hipMemcpyHostToDevice,
                                           sl.st));

@@ -10,16 +10,18 @@
 //                   bound; no MFMA.
 //   k_sizes_affine  var-size schemas with data-independent presence: the
 //                   scan telescopes, out_offsets[i] = i*C + sum_v(off_v[i] -
-//                   off_v[0]) — a pure map (encode_stream.inc)
+//                   off_v[0]) — a pure map (encode_var.inc)
 //   k_stream_sizes  other var-size schemas: blob sizes + decoupled look-back
-//                   scan -> out_offsets (encode_stream.inc)
-//   k_encode_stream var-size schemas: two bulk staging rounds into LDS, two
-//                   emitters per blob into an LDS image, 16-B stores
-//                   (encode_stream.inc)
-//   k_encode_var    per-blob fallback: one wavefront per blob; item sizes ->
-//                   wavefront prefix scan -> header words -> payload staged
-//                   in an LDS slot -> aligned 16-B stores
-//   k_decode        schema.DecodeBuffer semantics (SeqGetAccess + precheck),
+//                   scan -> out_offsets (encode_var.inc)
+//   k_encode_tiles  var-size schemas: one LDS-DMA load round, a compact LDS
+//                   frame image of every non-hole byte, then 16-B aligned
+//                   output chunks merging image bytes and HBM-resident long
+//                   values (encode_var.inc)
+//   k_encode_var    generic per-blob kernel (schemas past the tile plan's
+//                   tables): one wavefront per blob; item sizes -> wavefront
+//                   prefix scan -> header words -> payload staged in an LDS
+//                   slot -> aligned 16-B stores
+//   k_decode_win    schema.DecodeBuffer semantics (SeqGetAccess + precheck),
 //                   one thread per blob, exact error/panic reporting
 //   k_get_field     GetAccess random-field gather
 #include <hip/hip_runtime.h>
@@ -50,10 +52,6 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kSlot = 8192 + 64;      // LDS staging bytes per wavefront (k_encode_var)
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-// fixed-layout encode variant used when the caller does not pick one
-// (1..4: dword stores, 5..7: LDS re-staged 16-B stores; NT = non-temporal)
-constexpr int kDefaultFixedVariant = 2;
 
 __device__ __forceinline__ uint16_t enc_header(int64_t off, int tag) {
     return (uint16_t)((((uint64_t)off) << 3) & 0xFFFFu) | (uint16_t)(tag & 7);
@@ -162,7 +160,6 @@ __device__ __forceinline__ uint32_t lds_dword_at(const uint32_t* l32, uint32_t a
 // Lane-invariant form (B % 4 == 0): thread t owns output dword q = t % (B/4)
 // of blobs s, s+R, s+2R ... of the tile; its byte sources sit in registers.
 // Used for partial last tiles and shapes k_encode_fixed_tile does not take.
-template <bool NTS>
 __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCols cols, uint8_t* __restrict__ out,
                                                             uint64_t n, uint32_t* __restrict__ status,
                                                             uint32_t st_val) {
@@ -192,8 +189,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCol
                     v |= x;
                 }
             }
-            if (NTS) __builtin_nontemporal_store(v, o32 + (uint64_t)j * Q4);
-            else o32[(uint64_t)j * Q4] = v;
+            __builtin_nontemporal_store(v, o32 + (uint64_t)j * Q4);
         }
     }
     if (status)
@@ -238,11 +234,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_tile(FixProgram P, FixS
     const uint32_t lane = tid % kWave, wv = tid / kWave;
     const uint64_t blob0 = blockIdx.x * (uint64_t)T;  // full tiles only (the launcher sends
                                                       // a partial last tile to k_encode_fixed_dw)
-#ifndef ENC_ABL
-#define ENC_ABL 0
-#endif
     const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
-    for (int g = 0; g < (ENC_ABL == 2 ? 0 : S.n); g++) {
+    for (int g = 0; g < S.n; g++) {
         const uint32_t nch = (T * S.c[g].width) >> 4;
         const uint8_t* cbase = S.c[g].base + blob0 * S.c[g].width;
         for (uint32_t c0 = wv * kWave; c0 < nch; c0 += kBlock) {
@@ -262,7 +255,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_tile(FixProgram P, FixS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     uint32_t* l32 = (uint32_t*)lds;
-    if (nxi && ENC_ABL != 3) {
+    if (nxi) {
         auto assemble = [&](uint32_t i, const DwDesc& d) {
             const uint32_t j = i / (uint32_t)P.nx;
             uint32_t val = 0;
@@ -286,12 +279,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_tile(FixProgram P, FixS
 #pragma unroll
         for (int it = 0; it < PER; it++) {
             uint32_t val = cval;
-            if (ENC_ABL != 1) {
-                const uint32_t lo = l32[a >> 2], hi = l32[(a >> 2) + 1];
-                val |= __builtin_amdgcn_alignbyte(hi, lo, a) & xm;  // uses a & 3
-            } else {
-                val ^= a * 0x9E3779B1u + (uint32_t)blob0;  // ablation: data-dependent, no LDS read
-            }
+            const uint32_t lo = l32[a >> 2], hi = l32[(a >> 2) + 1];
+            val |= __builtin_amdgcn_alignbyte(hi, lo, a) & xm;  // uses a & 3
             a += xs;
             if (it & 1) asm volatile("" : "+v"(a));  // two iterations' reads in flight, no address table
             __builtin_nontemporal_store(val, o32);
@@ -372,9 +361,10 @@ __global__ void k_fill_offsets(uint64_t* offs, uint64_t n, uint64_t B) {
 // =========================================================================
 // variable-size encode
 // =========================================================================
-struct BlobCtx {
-    uint64_t present;   // container presence bits
-};
+// var offsets of either width (EncCols::off64 marks u64 columns)
+__device__ __forceinline__ uint64_t col_off(const EncCols& cols, int c, uint64_t i) {
+    return ((cols.off64 >> c) & 1ull) ? ((const uint64_t*)cols.off[c])[i] : (uint64_t)((const uint32_t*)cols.off[c])[i];
+}
 
 __device__ __forceinline__ uint64_t present_mask(const EncProgram& P, const EncCols& cols, uint64_t i) {
     uint64_t pm = 0;
@@ -401,10 +391,8 @@ __device__ __forceinline__ uint32_t item_size(const EncItem& it, const EncCols& 
                 if (v && !v[i]) { *slack += it.size; return 0; }
             }
             return it.size;
-        case IT_VAR: {
-            const uint32_t* o = cols.off[it.col];
-            return o[i + 1] - o[i];
-        }
+        case IT_VAR:
+            return (uint32_t)(col_off(cols, it.col, i + 1) - col_off(cols, it.col, i));
     }
     return 0;
 }
@@ -483,7 +471,7 @@ __device__ void var_blob_wave(const EncProgram& P, const EncCols& cols, uint64_t
         const uint8_t* src;
         if (it.type == IT_CONST) src = P.lits + it.lit;
         else if (it.type == IT_FIXED) src = cols.data[it.col] + i * (uint64_t)it.size;
-        else src = cols.data[it.col] + cols.off[it.col][i];
+        else src = cols.data[it.col] + col_off(cols, it.col, i);
         if (it.is_bool) {
             if (lane == 0) dst[p0] = src[0] != 0;
         } else {
@@ -528,728 +516,11 @@ __global__ __launch_bounds__(kBlock) void k_encode_var(EncProgram P, EncCols col
         var_blob_wave(P, cols, i, offs ? offs[i] : i * stride, out, cap, status, slot, pos, lane);
 }
 
-// Tiled var-size encode.  A workgroup takes VT consecutive blobs; their
-// outputs are contiguous in the arena (offsets from the size pass), so the
-// group assembles runs of blobs in LDS and writes them with 16-B stores.
-// Global-memory latency, not bandwidth, is what a per-blob design pays for,
-// so the kernel is organised in two rounds of independent loads:
-//   round 1  everything that depends only on kernel arguments, issued
-//            together: the schema program (items, header words, containers,
-//            literals), the tile's blob offsets, var-column offsets,
-//            validity bytes and every fixed column's rows (16-B chunks) —
-//            one flattened index space, kVBatch loads in flight per thread;
-//   round 2  the var columns' byte ranges (now known) are staged while the
-//            threads compute presence masks and item positions (LDS only);
-//   runs     the tile is split into runs (blobs whose start falls in one
-//            2^win_shift-byte window); per run the LDS buffer is zeroed,
-//            header words and items are written by (header|item, blob) pairs
-//            from LDS, and the run is stored with 16-B non-temporal stores;
-//   direct   var values that did not fit the staging budget (long values)
-//            are copied HBM->HBM afterwards, flattened over destination
-//            dwords so that every thread keeps several loads in flight.
-// Tiles outside the plan (offsets that disagree with the program, a blob
-// > 64 KiB, capacity overrun) and runs > bud bytes use var_blob_wave.
-constexpr int kVBatch = 4;
-constexpr int kVPFix = 32;     // plan limits (more -> one wavefront per blob)
-constexpr int kVPVar = 16;
-constexpr int kVPVal = 16;
-
-struct VarPlan {               // per-call plan, passed by value
-    int32_t nfix, nvar, nval, fix_bytes;
-    const uint8_t* fix_ptr[kVPFix];   // fixed leaf columns (one region per IT_FIXED item)
-    uint32_t fix_w[kVPFix];
-    uint32_t fix_lds[kVPFix];  // staging offset of fixed region r (full tile, 16-B aligned)
-    const uint32_t* var_off[kVPVar];  // var leaf columns (one per IT_VAR item)
-    const uint8_t* var_data[kVPVar];
-    int32_t var_item[kVPVar];
-    const uint8_t* val_ptr[kVPVal];   // validity columns passed by the caller
-    int8_t col_val[kMaxCols];  // column -> validity slot, -1 none
-};
-
-struct VVar {                  // var region of the current tile (LDS)
-    uint64_t src;              // column bytes of the tile's first blob
-    uint32_t lds_off;          // staging offset, UINT32_MAX = not staged
-    uint32_t pad;
-};
-
-struct VtLayout {
-    uint32_t boff, pmk, bst, misc, subs, items, ipk, ihr, hdrs, conts, lits, voff, vld, pos, vvar, fmis, freg, stg, total;
-};
-__host__ __device__ inline VtLayout vt_layout(int VT, const EncProgram& P, int nvar, int nval, uint32_t bud,
-                                               uint32_t in_bud) {
-    auto al16 = [](uint32_t x) { return (x + 15u) & ~15u; };
-    const uint32_t NI = (uint32_t)P.n_items;
-    VtLayout L;
-    uint32_t o = al16(bud + 32);
-    L.boff = o;  o += 8 * (VT + 1);
-    L.pmk = o;   o += 8 * VT;
-    L.bst = o;   o += 4 * VT;
-    L.misc = o;  o += 4 * 16;
-    L.subs = o;  o += al16(4 * (VT + 1));
-    L.items = o; o += al16(sizeof(EncItem) * NI);
-    L.ipk = o;   o += al16(4 * NI);
-    L.ihr = o;   o += al16(4 * NI);
-    L.hdrs = o;  o += al16(sizeof(EncHdr) * (uint32_t)P.n_hdrs);
-    L.conts = o; o += al16(sizeof(EncCont) * (uint32_t)P.n_conts);
-    L.lits = o;  o += al16((uint32_t)P.n_lits + 4);
-    L.voff = o;  o += 4 * nvar * (VT + 1);
-    L.vld = o;   o += al16(nval * VT);
-    L.pos = o;   o += al16(2 * VT * (NI + 1));
-    L.vvar = o;  o += al16(sizeof(VVar) * nvar);
-    L.fmis = o;  o += al16(4 * kVPFix);
-    L.freg = o;  o += 16 * kVPFix;
-    L.stg = o;   o += al16(in_bud + 16);
-    L.total = o;
-    return L;
-}
-
-
-__device__ __forceinline__ uint32_t magic_of(uint32_t d) {
-    return d > 1 ? (uint32_t)((0x100000000ull + d - 1) / d) : 0u;
-}
-__device__ __forceinline__ uint32_t fast_div(uint32_t t, uint32_t d, uint32_t mg) { return d > 1 ? __umulhi(t, mg) : t; }
-
 typedef __attribute__((address_space(1))) const uint32_t g_u32;
 typedef __attribute__((address_space(1))) const uint64_t g_u64;
 typedef __attribute__((address_space(1))) const uint8_t g_u8;
 
-template <int VT>
-__global__ __launch_bounds__(kBlock) void k_encode_var_tile(EncProgram P, EncCols cols, VarPlan V,
-                                                            const uint64_t* __restrict__ offs,
-                                                            uint8_t* __restrict__ out, uint64_t cap, uint64_t n,
-                                                            uint32_t* __restrict__ status, uint32_t bud,
-                                                            uint32_t win_shift, uint32_t in_bud,
-                                                            uint32_t* __restrict__ tflags, uint16_t* __restrict__ vpos,
-                                                            unsigned long long* __restrict__ prof) {
-    static_assert(VT % kWave == 0 && VT <= kBlock, "tile = whole wavefronts, at most one blob per thread");
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int NI = P.n_items, NP = NI + 1, NH = P.n_hdrs;
-    const VtLayout L = vt_layout(VT, P, V.nvar, V.nval, bud, in_bud);
-    uint8_t* obuf = lds;
-    uint64_t* boff = (uint64_t*)(lds + L.boff);
-    uint64_t* pmk = (uint64_t*)(lds + L.pmk);
-    uint32_t* bst = (uint32_t*)(lds + L.bst);
-    uint32_t* misc = (uint32_t*)(lds + L.misc);   // 0 fallback, 1 #runs, 4..7 wave counts, 8.. scratch
-    uint32_t* subs = (uint32_t*)(lds + L.subs);
-    EncItem* items = (EncItem*)(lds + L.items);
-    EncHdr* hdrs = (EncHdr*)(lds + L.hdrs);
-    EncCont* conts = (EncCont*)(lds + L.conts);
-    uint32_t* voff = (uint32_t*)(lds + L.voff);
-    uint8_t* vld = lds + L.vld;
-    uint16_t* pos = (uint16_t*)(lds + L.pos);
-    VVar* vvar = (VVar*)(lds + L.vvar);
-    uint32_t* fmis = (uint32_t*)(lds + L.fmis);
-    u32x4* freg = (u32x4*)(lds + L.freg);        // fixed region: {a0 lo, a0 hi, first chunk, LDS offset}
-    const uint32_t* ipk = (const uint32_t*)(lds + L.ipk);
-    const uint32_t* ihr = (const uint32_t*)(lds + L.ihr);
-    uint8_t* stg = lds + L.stg;
-
-    const uint64_t lo = (uint64_t)blockIdx.x * VT;
-    const uint32_t rows = (uint32_t)min((uint64_t)VT, n - lo);
-    uint64_t t_last = prof ? __builtin_amdgcn_s_memtime() : 0;
-    auto mark = [&](int ph) {
-        if (prof && tid == 0) {
-            const uint64_t t = __builtin_amdgcn_s_memtime();
-            atomicAdd(prof + ph, (unsigned long long)(t - t_last));
-            t_last = t;
-        }
-    };
-
-    // ---- round 1 -----------------------------------------------------------
-    // one flattened index space; the var-offset and validity segments are
-    // padded to whole wavefronts so the column behind an element is
-    // wave-uniform (scalar pointer loads, no dependent vector loads)
-    {
-        auto al64 = [](uint32_t x) { return (x + 63u) & ~63u; };
-        const uint32_t e_items = (uint32_t)NI * (sizeof(EncItem) / 4);
-        const uint32_t e_hdrs = e_items + (uint32_t)NH * (sizeof(EncHdr) / 4);
-        const uint32_t e_conts = e_hdrs + (uint32_t)P.n_conts * (sizeof(EncCont) / 4);
-        const uint32_t e_ipk = e_conts + (uint32_t)NI;
-        const uint32_t e_ihr = e_ipk + (uint32_t)NI;
-        const uint32_t e_lits = e_ihr + ((uint32_t)P.n_lits + 3) / 4;
-        const uint32_t e_boff = e_lits + rows + 1;
-        const uint32_t s_voff = al64(e_boff), S1 = al64(rows + 1);
-        const uint32_t e_voff = s_voff + (uint32_t)V.nvar * S1;
-        const uint32_t S0 = al64(rows);
-        const uint32_t e_vld = e_voff + (uint32_t)V.nval * S0;
-        // fixed-region table, once per workgroup (lane r of wave 0; prefix by scan)
-        if (wave == 0) {
-            uint32_t nch = 0;
-            uint64_t src = 0;
-            if (lane < V.nfix) {
-                src = (uint64_t)(uintptr_t)V.fix_ptr[lane] + lo * V.fix_w[lane];
-                nch = (uint32_t)(((src & 15) + (uint64_t)rows * V.fix_w[lane] + 15) >> 4);
-            }
-            const uint32_t incl = wave_incl_scan(nch, lane);
-            if (lane < V.nfix) {
-                freg[lane] = u32x4{(uint32_t)(src & ~15ull), (uint32_t)(src >> 32), incl - nch, V.fix_lds[lane]};
-                fmis[lane] = V.fix_lds[lane] + (uint32_t)(src & 15);
-            }
-            if (lane == 63) misc[15] = incl;
-        }
-        __syncthreads();
-        const uint32_t fix_ch = misc[15];
-        const uint32_t E = e_vld + fix_ch;
-        for (uint32_t e0 = tid; e0 < E; e0 += kVBatch * kBlock) {
-            u32x4 v[kVBatch];
-            uint32_t dst[kVBatch], kind[kVBatch];  // kind: 1 dword, 2 qword, 3 byte, 4 16-B chunk
-#pragma unroll
-            for (int m = 0; m < kVBatch; m++) {
-                const uint32_t e = e0 + m * kBlock;
-                kind[m] = 0;
-                dst[m] = 0;
-                v[m] = u32x4{0u, 0u, 0u, 0u};
-                if (e >= E) continue;
-                if (e < e_lits) {
-                    const uint32_t* src;
-                    uint32_t x;
-                    if (e < e_items) { src = (const uint32_t*)P.items; x = e; dst[m] = L.items + 4 * x; }
-                    else if (e < e_hdrs) { src = (const uint32_t*)P.hdrs; x = e - e_items; dst[m] = L.hdrs + 4 * x; }
-                    else if (e < e_conts) { src = (const uint32_t*)P.conts; x = e - e_hdrs; dst[m] = L.conts + 4 * x; }
-                    else if (e < e_ipk) { src = P.ipk; x = e - e_conts; dst[m] = L.ipk + 4 * x; }
-                    else if (e < e_ihr) { src = P.ihr; x = e - e_ipk; dst[m] = L.ihr + 4 * x; }
-                    else { src = (const uint32_t*)P.lits; x = e - e_ihr; dst[m] = L.lits + 4 * x; }
-                    v[m].x = ((g_u32*)src)[x];
-                    kind[m] = 1;
-                } else if (e < e_boff) {
-                    const uint32_t j = e - e_lits;
-                    const uint64_t o = ((g_u64*)offs)[lo + j];
-                    v[m].x = (uint32_t)o;
-                    v[m].y = (uint32_t)(o >> 32);
-                    dst[m] = L.boff + 8 * j;
-                    kind[m] = 2;
-                } else if (e < s_voff) {
-                    continue;
-                } else if (e < e_voff) {
-                    const uint32_t x = e - s_voff;
-                    const uint32_t vv = __builtin_amdgcn_readfirstlane(x / S1), j = x - vv * S1;
-                    if (j > rows) continue;
-                    v[m].x = ((g_u32*)V.var_off[vv])[lo + j];
-                    dst[m] = L.voff + 4 * (vv * (VT + 1) + j);
-                    kind[m] = 1;
-                } else if (e < e_vld) {
-                    const uint32_t x = e - e_voff;
-                    const uint32_t vv = __builtin_amdgcn_readfirstlane(x / S0), j = x - vv * S0;
-                    if (j >= rows) continue;
-                    v[m].x = ((g_u8*)V.val_ptr[vv])[lo + j];
-                    dst[m] = L.vld + vv * VT + j;
-                    kind[m] = 3;
-                } else {
-                    const uint32_t c = e - e_vld;
-                    u32x4 g = freg[0];
-                    for (int r = 1; r < V.nfix; r++) {
-                        const u32x4 h = freg[r];
-                        if (c >= h.z) g = h;
-                    }
-                    const uint64_t a0 = ((uint64_t)g.y << 32) | g.x;
-                    v[m] = *(const g_u32x4*)(uintptr_t)(a0 + 16ull * (c - g.z));
-                    dst[m] = L.stg + g.w + 16 * (c - g.z);
-                    kind[m] = 4;
-                }
-            }
-#pragma unroll
-            for (int m = 0; m < kVBatch; m++) {
-                switch (kind[m]) {
-                    case 1: *(uint32_t*)(lds + dst[m]) = v[m].x; break;
-                    case 2: *(uint64_t*)(lds + dst[m]) = ((uint64_t)v[m].y << 32) | v[m].x; break;
-                    case 3: lds[dst[m]] = (uint8_t)v[m].x; break;
-                    case 4: *(u32x4*)(lds + dst[m]) = v[m]; break;
-                    default: break;
-                }
-            }
-        }
-        if (tid < 8) misc[tid] = 0;  // misc[15] (fixed chunk count) stays
-    }
-    __syncthreads();
-    mark(0);
-    // ---- round 2: var staging plan + loads, positions while they fly --------
-    uint32_t any_direct = 0, vch = 0;
-    {
-        uint32_t used = (uint32_t)V.fix_bytes;
-        for (int vv = 0; vv < V.nvar; vv++) {
-            const uint32_t* vo = voff + vv * (VT + 1);
-            const uint64_t src = (uint64_t)(uintptr_t)(V.var_data[vv] + vo[0]);
-            const uint32_t bytes = vo[rows] - vo[0];
-            const uint32_t nch = bytes ? (uint32_t)(((src & 15) + bytes + 15) >> 4) : 0u;
-            const bool st = used + 16 * nch <= in_bud;
-            if (tid == 0) vvar[vv] = VVar{src, st ? used : UINT32_MAX, 0};
-            if (st) { used += 16 * nch; vch += nch; } else any_direct = 1;
-        }
-    }
-    u32x4 vb[kVBatch];
-    uint32_t vdst[kVBatch];
-    auto var_load = [&](uint32_t c0) {
-#pragma unroll
-        for (int m = 0; m < kVBatch; m++) {
-            const uint32_t c = c0 + m * kBlock;
-            uint64_t a0 = 0;
-            uint32_t cb = 0, base = 0, sl = 0, u2 = (uint32_t)V.fix_bytes;
-            for (int vv = 0; vv < V.nvar; vv++) {
-                const uint32_t* vo = voff + vv * (VT + 1);
-                const uint64_t src = (uint64_t)(uintptr_t)(V.var_data[vv] + vo[0]);
-                const uint32_t bytes = vo[rows] - vo[0];
-                const uint32_t nch = bytes ? (uint32_t)(((src & 15) + bytes + 15) >> 4) : 0u;
-                if (u2 + 16 * nch > in_bud) continue;  // not staged (same rule as the plan)
-                const bool in = c >= base;
-                a0 = in ? (src & ~15ull) : a0;
-                cb = in ? base : cb;
-                sl = in ? u2 : sl;
-                base += nch;
-                u2 += 16 * nch;
-            }
-            vdst[m] = sl + 16 * (c - cb);
-            if (c < vch) vb[m] = *(const g_u32x4*)(uintptr_t)(a0 + 16ull * (c - cb));
-        }
-    };
-    auto var_store = [&](uint32_t c0) {
-#pragma unroll
-        for (int m = 0; m < kVBatch; m++)
-            if (c0 + m * kBlock < vch) *(u32x4*)(stg + vdst[m]) = vb[m];
-    };
-    var_load(tid);
-    // presence masks and item positions (LDS only)
-    if (V.nval == 0) {
-        // no validity columns: every container and leaf is present, so an
-        // item's size is static or its var value's length
-        const uint64_t pm_all = P.n_conts >= 64 ? ~0ull : ((1ull << P.n_conts) - 1ull);
-        for (uint32_t j = tid; j < rows; j += kBlock) {
-            pmk[j] = pm_all;
-            bst[j] = 0;
-            uint32_t p = 0;
-            uint16_t* pj = pos + j * NP;
-            for (int k = 0; k < NI; k++) {
-                const uint32_t x = ipk[k], vs = (x >> 16) & 0xFFu;
-                uint32_t sz = x & 0xFFFFu;
-                if (vs != 0xFFu) {
-                    const uint32_t* vo = voff + vs * (VT + 1);
-                    sz = vo[j + 1] - vo[j];
-                    if (sz > 0xFFFFu) sz = 0x10000u;
-                }
-                pj[k] = (uint16_t)p;
-                p += sz;
-            }
-            pj[NI] = (uint16_t)p;
-            if (p > 0xFFFFu || boff[j + 1] - boff[j] != p || boff[j] + p > cap) atomicOr(&misc[0], 1u);
-        }
-    } else
-    for (uint32_t j = tid; j < rows; j += kBlock) {
-        uint64_t pm = 0;
-        for (int c = 0; c < P.n_conts; c++) {
-            const EncCont ct = conts[c];
-            bool p = ct.parent < 0 ? true : ((pm >> ct.parent) & 1ull);
-            if (p && ct.valid_col >= 0) {
-                const int vs = V.col_val[ct.valid_col];
-                if (vs >= 0) p = vld[vs * VT + j] != 0;
-            }
-            if (p) pm |= 1ull << c;
-        }
-        pmk[j] = pm;
-        bst[j] = 0;
-        uint32_t p = 0, slack = 0;
-        uint16_t* pj = pos + j * NP;
-        for (int k = 0; k < NI; k++) {
-            const EncItem it = items[k];
-            uint32_t sz = 0;
-            if ((pm >> it.cont) & 1ull) {
-                if (it.type == IT_VAR) {
-                    const uint32_t* vo = voff + it.vslot * (VT + 1);
-                    sz = vo[j + 1] - vo[j];
-                } else {
-                    sz = it.size;
-                    if (it.type == IT_FIXED && it.nullable) {
-                        const int vs = V.col_val[it.col];
-                        if (vs >= 0 && !vld[vs * VT + j]) { sz = 0; slack += it.size; }
-                    }
-                }
-            }
-            pj[k] = (uint16_t)p;
-            p += sz;
-            if (sz > 0xFFFFu) p = 0x10000u;  // forces the fallback below
-        }
-        pj[NI] = (uint16_t)p;
-        const uint32_t tot = p + (P.mode == PACKOS_MODE_PACKABLE ? slack : 0u);
-        if (p > 0xFFFFu || boff[j + 1] - boff[j] != tot || boff[j] + tot > cap) atomicOr(&misc[0], 1u);
-    }
-    var_store(tid);
-    for (uint32_t c0 = tid + kVBatch * kBlock; c0 < vch; c0 += kVBatch * kBlock) {
-        var_load(c0);
-        var_store(c0);
-    }
-    __syncthreads();
-    mark(1);
-    if (misc[0]) {  // outside the tile plan: one wavefront per blob, straight to HBM
-        if (tid == 0) tflags[blockIdx.x] = 0u;
-        uint32_t* wpos = (uint32_t*)obuf + wave * NP;
-        for (uint32_t j = wave; j < rows; j += kWavesPerBlock)
-            var_blob_wave(P, cols, lo + j, boff[j], out, cap, status, nullptr, wpos, lane);
-        return;
-    }
-    uint32_t* L32 = (uint32_t*)lds;
-    if (any_direct) {
-        // ---- direct mode (long unstaged values, e.g. C5): no run buffer.  One
-        // thread per blob streams the blob's non-value bytes (header words,
-        // fixed and literal items, staged values) to HBM: whole dwords with
-        // dword stores, dwords shared with a neighbour or a value hole byte by
-        // byte.  k_var_copy then fills the holes.
-        for (uint32_t j = tid; j < rows; j += kBlock) {
-            const uint16_t* pj = pos + j * NP;
-            const uint64_t g0 = boff[j];
-            uint64_t acc = 0, D = g0 >> 2;
-            uint32_t ph = (uint32_t)(g0 & 3), sb = ph, ovf = 0;
-            auto flush_part = [&](uint32_t hi) {
-                for (uint32_t y = sb; y < hi; y++) out[4 * D + y] = (uint8_t)(acc >> (8 * y));
-            };
-            auto put = [&](uint32_t v, uint32_t nb) {
-                acc |= (uint64_t)v << (8 * ph);
-                ph += nb;
-                if (ph >= 4) {
-                    if (sb == 0) *(uint32_t*)(out + 4 * D) = (uint32_t)acc;
-                    else flush_part(4);
-                    sb = 0;
-                    D++;
-                    acc >>= 32;
-                    ph -= 4;
-                }
-            };
-            for (int k = 0; k < NI; k++) {
-                const uint32_t p0 = pj[k], len = (uint32_t)(pj[k + 1] - p0);
-                if (len == 0) continue;
-                const EncItem it = items[k];
-                if (it.type == IT_HDR) {
-                    const uint32_t hr = ihr[k], hb = hr & 0xFFFFu, cnt = hr >> 16;
-                    for (uint32_t e = 0; e < cnt; e++) {
-                        const EncHdr h = hdrs[hb + e];
-                        uint16_t v;
-                        if (h.relative) {
-                            const int64_t off = (int64_t)pj[h.target] - (int64_t)(p0 + len);
-                            ovf |= off >= 8192;
-                            v = enc_header(off, h.tag);
-                        } else {
-                            v = h.value;
-                            ovf |= h.ovf != 0;
-                        }
-                        put(v, 2);
-                    }
-                    continue;
-                }
-                uint32_t so;
-                if (it.type == IT_CONST) {
-                    so = L.lits + it.lit;
-                } else if (it.type == IT_FIXED) {
-                    so = L.stg + fmis[it.reg] + j * it.size;
-                } else {
-                    const VVar g = vvar[it.vslot];
-                    const uint32_t* vo = voff + it.vslot * (VT + 1);
-                    if (g.lds_off == UINT32_MAX) {  // hole for k_var_copy
-                        if (ph > sb) flush_part(ph);
-                        const uint64_t dn = 4 * D + ph + len;
-                        D = dn >> 2;
-                        ph = sb = (uint32_t)(dn & 3);
-                        acc = 0;
-                        continue;
-                    }
-                    so = L.stg + g.lds_off + (uint32_t)(g.src & 15) + (vo[j] - vo[0]);
-                }
-                if (it.is_bool) {
-                    put(lds[so] != 0 ? 1u : 0u, 1);
-                    continue;
-                }
-                for (uint32_t x = 0; x < len; x += 4) {
-                    const uint32_t nb = min(4u, len - x);
-                    const uint32_t sa = so + x, wi = sa >> 2;
-                    uint32_t v = __builtin_amdgcn_alignbyte(L32[wi + 1], L32[wi], sa & 3);
-                    if (nb < 4) v &= (1u << (8 * nb)) - 1u;
-                    put(v, nb);
-                }
-            }
-            const uint32_t tot = (uint32_t)(boff[j + 1] - boff[j]);
-            for (uint32_t x = pj[NI]; x < tot; x += 4) put(0u, min(4u, tot - x));
-            if (ph > sb) flush_part(ph);
-            if (ovf) bst[j] |= 1u;
-        }
-        mark(2);
-    } else {
-    // ---- runs (everything staged, e.g. C3) --------------------------------------
-    {
-        const uint32_t j = tid;
-        const uint32_t win = j < rows ? (uint32_t)((boff[j] - boff[0]) >> win_shift) : 0u;
-        const uint32_t winp = (j > 0 && j < rows) ? (uint32_t)((boff[j - 1] - boff[0]) >> win_shift) : 0u;
-        const bool isnew = j < rows && (j == 0 || win != winp);
-        const uint64_t bal = __ballot(isnew);
-        if (lane == 0) misc[4 + wave] = (uint32_t)__popcll(bal);
-        __syncthreads();
-        uint32_t base = 0, tot = 0;
-        for (int w = 0; w < kWavesPerBlock; w++) {
-            base += w < wave ? misc[4 + w] : 0u;
-            tot += misc[4 + w];
-        }
-        if (isnew) subs[base + __popcll(bal & ((1ull << lane) - 1ull))] = j;
-        if (tid == 0) {
-            misc[1] = tot;
-            subs[tot] = rows;
-        }
-    }
-    __syncthreads();
-    mark(2);
-    const uint32_t nsub = misc[1];
-    for (uint32_t q = 0; q < nsub; q++) {
-        const uint32_t a = subs[q], b = subs[q + 1];
-        const uint64_t s0 = boff[a], s1 = boff[b];
-        const uint64_t al = s0 & ~15ull;
-        const uint32_t nb = (uint32_t)(s1 - al);
-        if (nb + 16 > bud) {
-            uint32_t* wpos = (uint32_t*)obuf + wave * NP;
-            for (uint32_t j = a + wave; j < b; j += kWavesPerBlock)
-                var_blob_wave(P, cols, lo + j, boff[j], out, cap, status, nullptr, wpos, lane);
-            for (uint32_t j = a + tid; j < b; j += kBlock) bst[j] = 2u;  // status written, bytes complete
-            __syncthreads();
-            continue;
-        }
-        const uint32_t nch = (nb + 15) >> 4;
-        for (uint32_t c = tid; c < nch; c += kBlock) ((u32x4*)obuf)[c] = u32x4{0u, 0u, 0u, 0u};
-        __syncthreads();
-        mark(5);
-        const uint32_t nbr = b - a, nb_mag = magic_of(nbr);
-        // header words: (header, blob) pairs, OR-ed into the zeroed buffer
-        for (uint32_t t = tid; t < nbr * (uint32_t)NH; t += kBlock) {
-            const uint32_t hh = fast_div(t, nbr, nb_mag), j = a + (t - hh * nbr);
-            const EncHdr h = hdrs[hh];
-            if (!((pmk[j] >> h.cont) & 1ull)) continue;
-            const uint16_t* pj = pos + j * NP;
-            const uint32_t hpos = pj[h.hdr_item];
-            uint16_t v;
-            bool ovf;
-            if (h.relative) {
-                const int64_t off = (int64_t)pj[h.target] - (int64_t)(hpos + items[h.hdr_item].size);
-                ovf = off >= 8192;
-                v = enc_header(off, h.tag);
-            } else {
-                v = h.value;
-                ovf = h.ovf != 0;
-            }
-            if (ovf) atomicOr(&bst[j], 1u);
-            const uint32_t d = (uint32_t)(boff[j] - al) + hpos + 2 * h.j;
-            const uint32_t sh = 8 * (d & 3);
-            if (sh <= 16) {
-                atomicOr(L32 + (d >> 2), (uint32_t)v << sh);
-            } else {
-                atomicOr(L32 + (d >> 2), ((uint32_t)v & 0xFFu) << 24);
-                atomicOr(L32 + (d >> 2) + 1, (uint32_t)v >> 8);
-            }
-        }
-        // items: (item, blob) pairs, item-major; whole destination dwords
-        // stored, partial ones OR-ed; sources funnel-shifted from LDS
-        for (uint32_t t = tid; t < nbr * (uint32_t)NI; t += kBlock) {
-            const uint32_t k = fast_div(t, nbr, nb_mag), j = a + (t - k * nbr);
-            const EncItem it = items[k];
-            if (it.type == IT_HDR) continue;
-            const uint16_t* pj = pos + j * NP;
-            const uint32_t p0 = pj[k], len = (uint32_t)(pj[k + 1] - p0);
-            if (len == 0) continue;
-            const uint32_t d = (uint32_t)(boff[j] - al) + p0;
-            uint32_t so;
-            if (it.type == IT_CONST) {
-                so = L.lits + it.lit;
-            } else if (it.type == IT_FIXED) {
-                so = L.stg + fmis[it.reg] + j * it.size;
-            } else {
-                const VVar g = vvar[it.vslot];
-                so = L.stg + g.lds_off + (uint32_t)(g.src & 15) + (voff[it.vslot * (VT + 1) + j] - voff[it.vslot * (VT + 1)]);
-            }
-            if (it.is_bool) {
-                atomicOr(L32 + (d >> 2), (uint32_t)(lds[so] != 0) << (8 * (d & 3)));
-                continue;
-            }
-            const uint32_t D0 = d >> 2, D1 = (d + len - 1) >> 2;
-            for (uint32_t D = D0; D <= D1; D++) {
-                const uint32_t sa = so + 4 * D - d;
-                const uint32_t wi = sa >> 2;
-                const uint32_t v = __builtin_amdgcn_alignbyte(L32[wi + 1], L32[wi], sa & 3);
-                const uint32_t b0 = 4 * D < d ? d - 4 * D : 0u, b1 = min(4u, d + len - 4 * D);
-                if (b0 == 0 && b1 == 4) {
-                    L32[D] = v;
-                } else {
-                    const uint32_t m = (b1 == 4 ? ~0u : ((1u << (8 * b1)) - 1u)) & ~((1u << (8 * b0)) - 1u);
-                    atomicOr(L32 + D, v & m);
-                }
-            }
-        }
-        __syncthreads();
-        mark(6);
-        // write [s0, s1)
-        for (uint32_t c = tid; c < nch; c += kBlock) {
-            const uint64_t g0 = al + 16ull * c;
-            if (g0 >= s0 && g0 + 16 <= s1) {
-                __builtin_nontemporal_store(((const u32x4*)obuf)[c], (u32x4*)(out + g0));
-            } else {
-                for (int x = 0; x < 16; x++) {
-                    const uint64_t gg = g0 + x;
-                    if (gg >= s0 && gg < s1) out[gg] = obuf[16 * c + x];
-                }
-            }
-        }
-        __syncthreads();
-        mark(7);
-    }
-    }
-    mark(3);
-    // ---- unstaged var values: hand their positions to k_var_copy -------------
-    if (tid == 0) {
-        uint32_t fl = 0;
-        for (int vv = 0; vv < V.nvar; vv++) fl |= (vvar[vv].lds_off == UINT32_MAX ? 1u : 0u) << vv;
-        tflags[blockIdx.x] = fl;
-    }
-    if (any_direct) {
-        for (int vv = 0; vv < V.nvar; vv++) {
-            if (vvar[vv].lds_off != UINT32_MAX) continue;
-            const int k = V.var_item[vv];
-            for (uint32_t j = tid; j < rows; j += kBlock)
-                vpos[(uint64_t)vv * n + lo + j] = (bst[j] & 2u) ? (uint16_t)0xFFFFu : pos[j * NP + k];
-        }
-    }
-    mark(4);
-    if (status)
-        for (uint32_t j = tid; j < rows; j += kBlock)
-            if (!(bst[j] & 2u)) status[lo + j] = (bst[j] & 1u) ? PACKOS_STATUS_OVERFLOW13 : 0u;
-}
-
-// Long var values the tile kernel did not stage: a flattened memmove per
-// tile over 16-B-aligned destination chunks, consecutive lanes on
-// consecutive chunks.  A chunk wholly inside one value takes two aligned 16-B
-// source loads, a funnel shift and one 16-B store; the (at most two) edge
-// chunks of a value go byte by byte.  Runs after k_encode_var_tile, which
-// skipped the whole chunks and wrote the edge chunks' other bytes.
-constexpr int kCopyBatch = 4;
-// (Measured on MI355X, C5: loading a whole chunk's source with one dwordx4
-// at a byte-misaligned address is 1.5x slower, at a dword-aligned address
-// 1.3x slower, than two 16-B-aligned loads + the funnel below.)
-
-__device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-    return q == 0 ? a : q == 1 ? b : q == 2 ? c : d;
-}
-
-template <int VT>
-__global__ __launch_bounds__(kBlock) void k_var_copy(VarPlan V, const uint64_t* __restrict__ offs,
-                                                     const uint32_t* __restrict__ tflags,
-                                                     const uint16_t* __restrict__ vpos, uint8_t* __restrict__ out,
-                                                     uint64_t n) {
-    __shared__ uint64_t boff[VT + 1];
-    __shared__ uint32_t vo[VT + 1], uo[VT + 1];
-    __shared__ uint16_t ps[VT];
-    __shared__ uint32_t wsum[kWavesPerBlock];
-    const uint32_t fl = tflags[blockIdx.x];
-    if (!fl) return;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t lo = (uint64_t)blockIdx.x * VT;
-    const uint32_t rows = (uint32_t)min((uint64_t)VT, n - lo);
-    for (uint32_t j = tid; j <= rows; j += kBlock) boff[j] = offs[lo + j];
-    for (int v = 0; v < V.nvar; v++) {
-        if (!((fl >> v) & 1u)) continue;
-        const uint32_t* voff_g = V.var_off[v];
-        for (uint32_t j = tid; j <= rows; j += kBlock) vo[j] = voff_g[lo + j];
-        for (uint32_t j = tid; j < rows; j += kBlock) ps[j] = vpos[(uint64_t)v * n + lo + j];
-        __syncthreads();
-        {
-            const uint32_t j = tid;
-            uint32_t cnt = 0;
-            if (j < rows && ps[j] != 0xFFFFu) {
-                const uint64_t d0 = boff[j] + ps[j];
-                const uint32_t len = vo[j + 1] - vo[j];
-                cnt = len ? (uint32_t)(((d0 + len + 15) >> 4) - (d0 >> 4)) : 0u;
-            }
-            const uint32_t incl = wave_incl_scan(cnt, lane);
-            if (lane == 63) wsum[wave] = incl;
-            __syncthreads();
-            uint32_t wb = 0, tot = 0;
-            for (int w = 0; w < kWavesPerBlock; w++) {
-                wb += w < wave ? wsum[w] : 0u;
-                tot += wsum[w];
-            }
-            if (j < rows) uo[j] = wb + incl - cnt;
-            if (tid == 0) uo[rows] = tot;
-            __syncthreads();
-        }
-        const uint32_t U = uo[rows];
-        const uint8_t* col = V.var_data[v];
-        // each wavefront takes 64 * kCopyBatch consecutive units per step; one
-        // (wave-uniform) binary search for the step's first unit, then each
-        // lane walks forward to its units' blobs
-        for (uint32_t ub = wave * (kWave * kCopyBatch); ub < U; ub += kWavesPerBlock * kWave * kCopyBatch) {
-            uint32_t jw;
-            {
-                uint32_t l = 0, r = rows - 1;  // last blob j with uo[j] <= ub
-                while (l < r) {
-                    const uint32_t mm = (l + r + 1) >> 1;
-                    if (uo[mm] <= ub) l = mm; else r = mm - 1;
-                }
-                jw = l;
-            }
-            u32x4 a[kCopyBatch], b[kCopyBatch];
-            uint64_t dst[kCopyBatch];
-            uint32_t sh[kCopyBatch], k0[kCopyBatch], k1[kCopyBatch];
-            uint32_t j = jw;
-#pragma unroll
-            for (int m = 0; m < kCopyBatch; m++) {
-                const uint32_t u = ub + lane + kWave * m;
-                k0[m] = k1[m] = 0;
-                sh[m] = 0;
-                dst[m] = 0;
-                a[m] = b[m] = u32x4{0u, 0u, 0u, 0u};
-                if (u >= U) continue;
-                while (uo[j + 1] <= u) j++;
-                const uint64_t d0 = boff[j] + ps[j];
-                const uint32_t ln = vo[j + 1] - vo[j];
-                const uint64_t C = 16 * ((d0 >> 4) + (u - uo[j]));
-                dst[m] = C;
-                k0[m] = C >= d0 ? 0u : (uint32_t)(d0 - C);
-                k1[m] = (uint32_t)min((uint64_t)16, d0 + ln - C);
-                const uintptr_t xa = (uintptr_t)(col + vo[j]) + (uintptr_t)(C - d0);
-                // aligned blocks holding needed bytes only (edge chunks may need one)
-                const g_u32x4* xw = (const g_u32x4*)(xa & ~(uintptr_t)15);
-                sh[m] = (uint32_t)(xa & 15);
-                if (k0[m] < 16 - sh[m]) a[m] = xw[0];
-                if (sh[m] && k1[m] > 16 - sh[m]) b[m] = xw[1];
-            }
-#pragma unroll
-            for (int m = 0; m < kCopyBatch; m++) {
-                if (k1[m] <= k0[m]) continue;
-                u32x4 o4;
-                if (sh[m] == 0) {
-                    o4 = a[m];
-                } else {
-                    const uint32_t q = sh[m] >> 2, sb = sh[m] & 3;
-                    const uint32_t w[8] = {a[m].x, a[m].y, a[m].z, a[m].w, b[m].x, b[m].y, b[m].z, b[m].w};
-                    uint32_t t5[5];
-#pragma unroll
-                    for (int i = 0; i < 5; i++) t5[i] = sel4(q, w[i], w[i + 1], w[i + 2], w[i + 3]);
-                    o4.x = __builtin_amdgcn_alignbyte(t5[1], t5[0], sb);
-                    o4.y = __builtin_amdgcn_alignbyte(t5[2], t5[1], sb);
-                    o4.z = __builtin_amdgcn_alignbyte(t5[3], t5[2], sb);
-                    o4.w = __builtin_amdgcn_alignbyte(t5[4], t5[3], sb);
-                }
-                if (k0[m] == 0 && k1[m] == 16) {
-                    __builtin_nontemporal_store(o4, (u32x4*)(out + dst[m]));
-                } else {
-                    const uint32_t wv[4] = {o4.x, o4.y, o4.z, o4.w};
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        const uint32_t lo4 = 4 * i, s4 = max(k0[m], lo4), e4 = min(k1[m], lo4 + 4);
-                        if (s4 >= e4) continue;
-                        if (s4 == lo4 && e4 == lo4 + 4) {
-                            *(uint32_t*)(out + dst[m] + lo4) = wv[i];
-                        } else {
-                            for (uint32_t y = s4; y < e4; y++) out[dst[m] + y] = (uint8_t)(wv[i] >> (8 * (y - lo4)));
-                        }
-                    }
-                }
-            }
-        }
-        __syncthreads();
-    }
-}
-
-#include "encode_stream.inc"
+#include "encode_var.inc"
 
 // =========================================================================
 // decode: schema.DecodeBuffer, one thread per blob
@@ -1453,17 +724,6 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
     return sv;
 }
 
-// generic decode: one thread per blob
-__global__ __launch_bounds__(kBlock) void k_decode(DecProgram P, DecCols cols, const uint8_t* __restrict__ arena,
-                                                   const uint64_t* __restrict__ offs, uint64_t stride, uint64_t n,
-                                                   uint32_t* __restrict__ status) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t a0 = offs ? offs[i] : i * stride;
-    const uint64_t a1 = offs ? offs[i + 1] : (i + 1) * stride;
-    status[i] = decode_blob(P, cols, GReader{arena}, a0, a1, i);
-}
-
 // Generic decode with a per-blob LDS window: every thread first fetches its
 // blob's first kDecWinChunks x 16 bytes (header block, leading fields) with
 // 16-B loads, all in flight, then runs decode_blob reading the window and
@@ -1582,7 +842,14 @@ __global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecPro
     for (uint32_t j = tid; j < rows; j += kBlock) fail[j] = 0;
     // 1. stage: global -> LDS with global_load_lds_dwordx4 (every chunk of the
     //    tile in flight at once; a load -> ds_write loop waits per chunk)
-    const uint32_t bytes = rows * B;
+    //    Staged bytes stop at the tile's end offset: a truncated or corrupt
+    //    batch must not read past what its offsets cover (the tile then fails
+    //    the contiguity check and takes the per-blob path below).
+    uint32_t bytes = rows * B;
+    if (offs) {
+        const uint64_t end = ((c_u64*)(uintptr_t)offs)[blob0 + rows];
+        bytes = end <= base ? 0u : (uint32_t)min((uint64_t)bytes, end - base);
+    }
     if (aligned_base) {
         const uint8_t* src = arena + base;
         const uint32_t n16 = bytes >> 4, lane = tid & 63, c00 = tid & ~63u;
@@ -1714,14 +981,22 @@ struct PathArg {
     int32_t p[16];
 };
 
+// One thread per blob: walk the nested path (GetNestedGetAccess, get.go:377-
+// 401), then apply one Get* family (see packos_get_batch in packos.h) and
+// optionally gather the typed value into a dense output row.
 __global__ __launch_bounds__(kBlock) void k_get_field(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
-                                                      uint64_t stride, uint64_t n, PathArg path, int depth, int want_tag, int want_width, uint64_t* out_start,
-                                                      uint32_t* out_len, uint8_t* out_tag, uint8_t* status) {
+                                                      uint64_t stride, uint64_t n, PathArg path, int depth, int getter,
+                                                      int want_tag, int want_width, uint8_t* __restrict__ out_values,
+                                                      uint32_t value_width, uint64_t* out_start, uint32_t* out_len,
+                                                      uint8_t* out_tag, uint8_t* status) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t a0 = offs ? offs[i] : i * stride;
     const uint64_t a1 = offs ? offs[i + 1] : (i + 1) * stride;
     out_start[i] = 0; out_len[i] = 0; out_tag[i] = 0;
+    uint8_t* dst = out_values ? out_values + i * value_width : nullptr;
+    if (dst)
+        for (uint32_t k = 0; k < value_width; k++) dst[k] = 0;
     DGet g;
     if (!dget_init(g, arena, a0, (int64_t)(a1 - a0))) { status[i] = 3; return; }
     int tp; int64_t s, e;
@@ -1735,11 +1010,37 @@ __global__ __launch_bounds__(kBlock) void k_get_field(const uint8_t* __restrict_
     }
     dget_range(g, arena, path.p[depth - 1], tp, s, e);
     out_tag[i] = (uint8_t)tp;
-    const bool ok = want_width >= 0 ? (tp == want_tag && e - s == want_width) : (tp == want_tag && e >= s);
-    if (!ok) { status[i] = 1; return; }
-    out_start[i] = g.start + (uint64_t)s;
-    out_len[i] = (uint32_t)(e - s);
-    status[i] = 0;
+    const int64_t w = e - s;
+    int r = 0;
+    switch (getter) {
+        case PACKOS_GET_NULLABLE:
+            if (w == 0) { r = 4; break; }
+            [[fallthrough]];
+        case PACKOS_GET_FIXED: r = (tp != want_tag || w != want_width); break;
+        case PACKOS_GET_SPAN: r = (tp != want_tag || e < s); break;
+        case PACKOS_GET_INT:
+            r = tp != PACKOS_TAG_INTEGER ? 1 : w == 0 ? 4 : (w != 1 && w != 2 && w != 4 && w != 8);
+            break;
+        case PACKOS_GET_FLOAT: r = tp != PACKOS_TAG_FLOATING ? 1 : w == 0 ? 4 : (w != 4 && w != 8); break;
+        default: r = 1;
+    }
+    status[i] = (uint8_t)r;
+    if (r) return;
+    const uint64_t at = g.start + (uint64_t)s;
+    out_start[i] = at;
+    out_len[i] = (uint32_t)w;
+    if (!dst || getter == PACKOS_GET_SPAN) return;
+    const uint8_t* src = arena + at;
+    if (getter == PACKOS_GET_INT) {
+        uint64_t v = 0;
+        for (int k = 0; k < w; k++) v |= (uint64_t)src[k] << (8 * k);
+        if (w < 8 && ((v >> (8 * w - 1)) & 1)) v |= ~0ull << (8 * w);
+        for (uint32_t k = 0; k < 8 && k < value_width; k++) dst[k] = (uint8_t)(v >> (8 * k));
+    } else if (tp == PACKOS_TAG_BOOL && w == 1) {
+        dst[0] = src[0] != 0;
+    } else {
+        for (int64_t k = 0; k < w && k < (int64_t)value_width; k++) dst[k] = src[k];
+    }
 }
 
 // =========================================================================
@@ -1800,7 +1101,12 @@ int fill_enc_cols(const packos_schema* s, const packos_column* cols, EncCols& ec
     for (size_t c = 0; c < s->col_node.size(); c++) {
         const Node& n = s->nodes[s->col_node[c]];
         ec.data[c] = (const uint8_t*)cols[c].data;
-        ec.off[c] = cols[c].offsets;
+        if (cols[c].offsets64) {
+            ec.off[c] = cols[c].offsets64;
+            ec.off64 |= 1ull << c;
+        } else {
+            ec.off[c] = cols[c].offsets;
+        }
         ec.valid[c] = cols[c].valid;
         bool scalar = n.kind >= K_INT && n.kind <= K_BOOL;
         bool fixed_str = (n.kind == K_STRING || n.kind == K_BYTES) && n.width > 0;
@@ -1890,7 +1196,6 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     t.dfix.B = (int)s->all_present_size;
     t.dfix.T = s->fix_T;
     t.dfix.n_cols = (int)s->dfix.size();
-    t.dfix.total_units = s->dfix_units;
     {
         const uint64_t q = (uint64_t)std::max<int64_t>(1, s->all_present_size / 4);
         const uint64_t bb = (uint64_t)std::max<int64_t>(2, s->all_present_size);
@@ -1919,236 +1224,61 @@ void packos_schema_free(packos_schema* s) {
     delete s;
 }
 
-// [scan tile sums][tile flags (k_var_copy)][value positions (u16, per var leaf x blob)]
-// (the scan tile sums also hold k_encode_stream's ticket + per-256-blob look-back words)
-static size_t ws_scan_bytes(size_t n) { return (((n + kS2T - 1) / kS2T) + 16) * sizeof(uint64_t); }
-static size_t ws_flag_bytes(size_t n) { return ((n + 63) / 64 + 4) * sizeof(uint32_t); }
+// workspace: [look-back ticket + one word per k_stream_sizes tile]
+static size_t ws_scan_bytes(size_t n) { return (((n + kSzTile - 1) / kSzTile) + 16) * sizeof(uint64_t); }
 
 size_t packos_encode_workspace_size(const packos_schema* s, size_t n_blobs) {
-    size_t nvar = 0;
-    if (s)
-        for (const EncItem& it : s->items) nvar += it.type == IT_VAR;
-    const size_t a = (ws_scan_bytes(n_blobs) + 255) & ~(size_t)255;
-    const size_t b = (ws_flag_bytes(n_blobs) + 255) & ~(size_t)255;
-    return a + b + nvar * n_blobs * sizeof(uint16_t) + 256;
+    (void)s;
+    return ((ws_scan_bytes(n_blobs) + 255) & ~(size_t)255) + 256;
+}
+
+// data-independent presence: out_offsets has a closed form (k_sizes_affine)
+static bool affine_layout(const packos_schema* s, const EncCols& ec, AffPlan* A) {
+    AffPlan a{};
+    if (s->tune.sizes_scan) return false;
+    for (const EncCont& c : s->conts)
+        if (c.valid_col >= 0 && ec.valid[c.valid_col]) return false;
+    for (const EncItem& it : s->items) {
+        if (it.type == IT_VAR) {
+            if (a.nv == kAffVar) return false;
+            if ((ec.off64 >> it.col) & 1ull) a.w8 |= 1u << a.nv;
+            a.off[a.nv++] = ec.off[it.col];
+        } else {
+            if (it.type == IT_FIXED && it.nullable && ec.valid[it.col] && s->mode != PACKOS_MODE_PACKABLE) return false;
+            a.C += it.size;
+        }
+    }
+    if (A) *A = a;
+    return true;
 }
 
 static int size_pass(packos_schema* s, DeviceTables* t, const EncCols& ec, size_t n, uint64_t* offs, void* ws,
                      size_t ws_bytes, hipStream_t st) {
     if (!offs) { set_error("out_offsets required for a variable-size schema"); return PACKOS_E_INVALID; }
-    if (!ws || ws_bytes < packos_encode_workspace_size(s, n)) {
-        set_error("workspace too small");
-        return PACKOS_E_WORKSPACE;
-    }
     if (n == 0) {
         HIP_TRY(hipMemsetAsync(offs, 0, sizeof(uint64_t), st));
         return PACKOS_OK;
     }
-    // data-independent presence: closed-form sizes (k_sizes_affine), no scan
-    {
-        AffPlan A{};
-        bool affine = getenv("PACKOS_SIZES_SCAN") == nullptr;
-        for (const EncCont& c : s->conts) affine &= c.valid_col < 0 || ec.valid[c.valid_col] == nullptr;
-        for (const EncItem& it : s->items) {
-            if (!affine) break;
-            if (it.type == IT_VAR) {
-                if (A.nv == kAffVar) affine = false;
-                else A.off[A.nv++] = ec.off[it.col];
-            } else {
-                if (it.type == IT_FIXED && it.nullable && ec.valid[it.col] && s->mode != PACKOS_MODE_PACKABLE)
-                    affine = false;
-                A.C += it.size;
-            }
-        }
-        if (affine) {
-            const uint64_t per = (uint64_t)kBlock * kAffPer;
-            hipLaunchKernelGGL(k_sizes_affine, dim3((unsigned)((n + 1 + per - 1) / per)), dim3(kBlock), 0, st, A,
-                               offs, (uint64_t)n);
-            HIP_TRY(hipGetLastError());
-            return PACKOS_OK;
-        }
+    AffPlan A;
+    if (affine_layout(s, ec, &A)) {
+        const uint64_t per = (uint64_t)kBlock * kAffPer;
+        hipLaunchKernelGGL(k_sizes_affine, dim3((unsigned)((n + 1 + per - 1) / per)), dim3(kBlock), 0, st, A,
+                           offs, (uint64_t)n);
+        HIP_TRY(hipGetLastError());
+        return PACKOS_OK;
+    }
+    if (!ws || ws_bytes < packos_encode_workspace_size(s, n)) {
+        set_error("workspace too small");
+        return PACKOS_E_WORKSPACE;
     }
     // k_stream_sizes: ticket + per-tile look-back words at the start of ws
     const uint64_t ntiles = (n + kSzTile - 1) / kSzTile;
     HIP_TRY(hipMemsetAsync(ws, 0, (ntiles + 1) * sizeof(uint64_t), st));
-    static unsigned long long* zprof = nullptr;  // debug: PACKOS_STREAM_PROF=1 prints phase clocks
-    const bool want_prof = getenv("PACKOS_STREAM_PROF") != nullptr;
-    if (want_prof && !zprof) HIP_TRY(hipMalloc(&zprof, 16 * sizeof(unsigned long long)));
-    if (want_prof) HIP_TRY(hipMemsetAsync(zprof, 0, 16 * sizeof(unsigned long long), st));
     hipLaunchKernelGGL(k_stream_sizes, dim3((unsigned)ntiles), dim3(kBlock),
                        sizes_lds_bytes((int)s->items.size(), (int)s->conts.size()), st, t->enc, ec, (uint64_t*)ws,
-                       offs, (uint64_t)n, want_prof ? zprof : nullptr);
+                       offs, (uint64_t)n);
     HIP_TRY(hipGetLastError());
-    if (want_prof) {
-        unsigned long long h[16];
-        HIP_TRY(hipMemcpyAsync(h, zprof, sizeof(h), hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        fprintf(stderr, "sizes tiles=%llu clocks/tile:", (unsigned long long)ntiles);
-        for (int i = 0; i < 5; i++) fprintf(stderr, " p%d=%.0f", i, (double)h[8 + i] / ntiles);
-        fprintf(stderr, "\n");
-    }
     return PACKOS_OK;
-}
-
-// k_encode_stream plan for one call (kernel argument).  false: the schema /
-// columns exceed the plan's tables or LDS, use the tiled encoder.
-static bool stream_plan(const packos_schema* s, const EncCols& ec, S2Plan& S) {
-    memset(&S, 0, sizeof(S));
-    const uint32_t NI = (uint32_t)s->items.size();
-    if (NI > (uint32_t)kS2Items || s->conts.size() > (size_t)kS2Conts) return false;
-    // value staging (fix_cap / var_cap) is off by default: measured on the box, the LDS it
-    // takes costs more occupancy than the HBM latency it hides (C3 0.162 -> 0.132 ms)
-    uint32_t longv = 48, img_cap = 14336, fix_cap = 0, var_cap = 0, var_per = 36;
-    if (const char* e = getenv("PACKOS_STREAM_LONG")) longv = (uint32_t)std::max(32, std::min(4096, atoi(e)));
-    if (const char* e = getenv("PACKOS_STREAM_IMG")) img_cap = (uint32_t)std::max(2048, std::min(49152, atoi(e)));
-    if (const char* e = getenv("PACKOS_STREAM_VAR")) var_cap = (uint32_t)std::max(0, std::min(32768, atoi(e)));
-    if (const char* e = getenv("PACKOS_STREAM_FIX")) fix_cap = (uint32_t)std::max(0, std::min(49152, atoi(e)));
-    if (const char* e = getenv("PACKOS_STREAM_VPER")) var_per = (uint32_t)std::max(4, std::min(256, atoi(e)));
-    auto al16 = [](uint32_t x) { return (x + 15u) & ~15u; };
-    uint32_t o = 0, cb = 0;
-    std::vector<int> val_seg(kMaxCols, -1), fix_seg(kMaxCols, -1), off_seg(kMaxCols, -1), var_slot(kMaxCols, -1);
-    auto add_seg = [&](const uint8_t* src, uint32_t w, bool extra) -> int {
-        if (S.nseg >= kS2Seg) return -1;
-        const int k = S.nseg++;
-        const uint32_t bytes = (uint32_t)(kS2T + (extra ? 1 : 0)) * w;
-        const uint32_t maxch = (bytes + 15) / 16 + 1;
-        S.seg_src[k] = src;
-        S.seg_w[k] = w;
-        S.seg_lds[k] = o;
-        S.seg_cb[k] = cb;
-        if (extra) S.seg_extra |= 1u << k;
-        cb += maxch;
-        o += maxch * 16 + 16;   // +16: padding for 2-dword unaligned reads
-        return k;
-    };
-    // validity columns, var offsets, fixed columns (up to fix_cap bytes per tile)
-    for (size_t c = 0; c < s->col_node.size() && c < (size_t)kMaxCols; c++) {
-        if (!ec.valid[c]) continue;
-        if ((val_seg[c] = add_seg(ec.valid[c], 1, false)) < 0) return false;
-    }
-    uint32_t fix_bytes = 0, worst = 0;
-    for (const EncItem& it : s->items) {
-        if (it.type == IT_VAR) {
-            if (off_seg[it.col] < 0 && (off_seg[it.col] = add_seg((const uint8_t*)ec.off[it.col], 4, true)) < 0)
-                return false;
-            worst += longv;
-            continue;
-        }
-        worst += it.type == IT_HDR ? it.size : std::min(it.size, longv);
-        if (it.type != IT_FIXED || fix_seg[it.col] >= 0) continue;
-        if (fix_bytes + kS2T * it.size <= fix_cap && S.nseg < kS2Seg) {
-            fix_seg[it.col] = add_seg(ec.data[it.col], it.size, false);
-            fix_bytes += kS2T * it.size;
-        }
-    }
-    S.seg_cb[S.nseg] = cb;
-    // var columns staged in the same load round (their tile range known from
-    // two uniform offset loads)
-    uint32_t vb = 0;
-    for (const EncItem& it : s->items) {
-        if (it.type != IT_VAR || var_slot[it.col] >= 0 || S.nvar >= kS2Var) continue;
-        const uint32_t bud = std::min<uint32_t>(al16(kS2T * var_per + 32), var_cap > vb ? var_cap - vb : 0);
-        if (bud < 512) break;
-        const int k = S.nvar++;
-        var_slot[it.col] = k;
-        S.var_off[k] = ec.off[it.col];
-        S.var_data[k] = ec.data[it.col];
-        S.var_lds[k] = o;
-        S.var_bud[k] = bud;
-        S.var_cb[k] = vb / 16;
-        vb += bud;
-        o += bud + 16;
-    }
-    S.var_cb[S.nvar] = vb / 16;
-    // per-item plan
-    uint32_t nlong = 0;
-    for (uint32_t k = 0; k < NI; k++) {
-        const EncItem& it = s->items[k];
-        S2K& x = S.item[k];
-        x.type = it.type;
-        x.size = (uint16_t)std::min<uint32_t>(it.size, 0xFFFFu);
-        x.cont = (uint16_t)it.cont;
-        x.col = it.col;
-        x.flags = it.is_bool ? SD_BOOL : 0;
-        if (it.type == IT_HDR) {
-            x.la = (uint16_t)(s->ihr[k] & 0xFFFFu);
-            x.lv = (uint16_t)(s->ihr[k] >> 16);
-        } else if (it.type == IT_CONST) {
-            if (it.lit > 0xFFFFu) return false;
-            x.la = (uint16_t)it.lit;
-            if (it.size > longv) { x.flags |= SD_LONG; nlong++; }
-        } else if (it.type == IT_FIXED) {
-            const int sg = fix_seg[it.col];
-            if (sg >= 0) {
-                x.la = (uint16_t)S.seg_lds[sg];
-                x.src15 = (uint8_t)((uintptr_t)ec.data[it.col] & 15);
-                x.flags |= SD_STAGED;
-                if (it.size == 1 || it.size == 2 || it.size == 4 || it.size == 8) x.flags |= SD_DIRECT;
-            }
-            else if ((it.size == 1 || it.size == 2 || it.size == 4 || it.size == 8) &&
-                     ((uintptr_t)ec.data[it.col] % it.size) == 0)
-                x.flags |= SD_GDIRECT;
-            if (!(x.flags & (SD_DIRECT | SD_GDIRECT)) && it.size > longv) { x.flags |= SD_LONG; nlong++; }
-            if (it.nullable && val_seg[it.col] >= 0) {
-                x.flags |= SD_VALID;
-                x.lv = (uint16_t)S.seg_lds[val_seg[it.col]];
-                x.vsrc15 = (uint8_t)((uintptr_t)ec.valid[it.col] & 15);
-            }
-        } else {
-            const int sg = off_seg[it.col];
-            x.la = (uint16_t)S.seg_lds[sg];
-            x.src15 = (uint8_t)((uintptr_t)ec.off[it.col] & 15);
-            x.flags |= SD_LONG;
-            nlong++;
-            if (var_slot[it.col] >= 0) { x.flags |= SD_VSLOT; x.lv = (uint16_t)var_slot[it.col]; }
-        }
-    }
-    for (size_t c = 0; c < s->conts.size(); c++) {
-        const EncCont& ct = s->conts[c];
-        S2KCont& x = S.cont[c];
-        x.parent = ct.parent;
-        x.lv = 0xFFFFu;
-        if (ct.valid_col >= 0 && val_seg[ct.valid_col] >= 0) {
-            x.lv = (uint16_t)S.seg_lds[val_seg[ct.valid_col]];
-            x.vsrc15 = (uint8_t)((uintptr_t)ec.valid[ct.valid_col] & 15);
-        }
-    }
-    S.pos_lds = o;
-    o += al16(2u * kS2T * (NI + 1));
-    uint32_t img = (uint32_t)std::min<uint64_t>(img_cap, (uint64_t)kS2T * worst + 32);
-    img = std::max<uint32_t>(img, std::max<uint32_t>(2048u, 16u * (NI + 1) * kWavesPerBlock));
-    S.img_bytes = al16(img);
-    S.img_lds = o;
-    o += S.img_bytes + 16;
-    S.hole_cap = std::min<uint32_t>(nlong * kS2T, 1024u);
-    S.hole_lds = o;
-    o += al16(4 * S.hole_cap + 4 * (S.hole_cap + 2) + 8 * S.hole_cap);
-    S.blob_lds = o;
-    o += al16((uint32_t)sizeof(S2Blob) * kS2T);
-    S.desc_lds = o;
-    o += (uint32_t)sizeof(S2Desc) * NI;
-    S.hdr_lds = o;
-    o += al16((uint32_t)sizeof(S2Hdr) * (uint32_t)s->hdrs.size());
-    S.hw_lds = o;
-    o += al16(2u * kS2T * (uint32_t)s->hdrs.size()) + 16;
-    S.grp_lds = o;
-    o += S.hole_cap ? 2u * kS2Grp : 0u;
-    S.misc_lds = o;
-    o += 64;
-    S.lds_total = o;
-    S.longv = longv;
-    // emitter split: the item boundary closest to half the estimated blob bytes
-    uint64_t tot = 0;
-    for (const EncItem& it : s->items) tot += it.type == IT_VAR ? 32u : it.size;
-    uint64_t run = 0, best = ~0ull;
-    S.mid = NI;
-    for (uint32_t k = 0; k <= NI; k++) {
-        const uint64_t d = 2 * run > tot ? 2 * run - tot : tot - 2 * run;
-        if (d < best) { best = d; S.mid = k; }
-        if (k < NI) run += s->items[k].type == IT_VAR ? 32u : s->items[k].size;
-    }
-    if (const char* e = getenv("PACKOS_STREAM_MID")) S.mid = (uint32_t)std::max(0, std::min((int)NI, atoi(e)));
-    return o <= 64 * 1024;
 }
 
 int packos_encoded_size_batch(const packos_schema* cs, const packos_column* cols, size_t n, uint64_t* out_offsets,
@@ -2177,7 +1307,10 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
                         void* stream) {
     packos_schema* s = const_cast<packos_schema*>(cs);
     if (!s || !cols || (!out && n)) { set_error("packos_encode_batch: bad argument"); return PACKOS_E_INVALID; }
-    if (n == 0) return PACKOS_OK;
+    if (n == 0) {
+        if (out_offsets) HIP_TRY(hipMemsetAsync(out_offsets, 0, sizeof(uint64_t), (hipStream_t)stream));
+        return PACKOS_OK;
+    }
     int dev, r;
     if ((r = current_device(&dev))) return r;
     DeviceTables* t;
@@ -2207,9 +1340,10 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
             const bool tile_ok = dw_ok && B >= 16 && (int)s->fcols.size() <= kStageCols &&
                                  (uint32_t)s->fix_T == 16u * (kBlock / (uint32_t)(B / 4)) &&
                                  s->fix_tile_lds <= 64 * 1024;
-            if (variant == 0) variant = tile_ok ? 13 : dw_ok ? kDefaultFixedVariant : 8;
-            if (variant == 13 && !tile_ok) variant = dw_ok ? kDefaultFixedVariant : 8;
-            if ((variant == 1 || variant == 2) && !dw_ok) variant = 8;
+            if (variant == 0) variant = tile_ok ? 13 : dw_ok ? 2 : 8;
+            if (variant == 13 && !tile_ok) variant = dw_ok ? 2 : 8;
+            if (variant == 2 && !dw_ok) variant = 8;
+            if (variant != 2 && variant != 13) variant = 8;
             const size_t fcb = ((s->fcols.size() * kLFixBytes) + 15) / 16 * 16;
             // each kernel gets the column table copied right after the LDS it uses
             FixProgram pdw = t->fix, pgen = t->fix;
@@ -2217,34 +1351,30 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
             const size_t gen_tables = (size_t)s->fix_lds + ((B + 1) * 4 + 15) / 16 * 16 + s->fsegs.size() * sizeof(FixSeg);
             pgen.fc_lds = (int32_t)gen_tables;
             const size_t lds_dw = (size_t)pdw.fc_lds + fcb;
-            switch (variant) {
-                case 1: hipLaunchKernelGGL((k_encode_fixed_dw<false>), dim3((unsigned)tiles), dim3(kBlock), lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
-                case 2: hipLaunchKernelGGL((k_encode_fixed_dw<true>), dim3((unsigned)tiles), dim3(kBlock), lds_dw, st, pdw, ec, out, (uint64_t)n, status, stv); break;
-                case 13: {
-                    FixStage S;
-                    memset(&S, 0, sizeof(S));
-                    S.n = (int32_t)s->fcols.size();
-                    for (int k = 0; k < S.n; k++) {
-                        const FixCol& fc = s->fcols[k];
-                        S.c[k] = FixStageCol{ec.data[fc.col], fc.width, fc.lds_off, fc.chunk_begin, fc.flags};
-                        S.flags |= (int32_t)(fc.flags & 1u);
-                    }
-                    const uint64_t full = n / s->fix_T, rem = n - full * s->fix_T;
-                    if (full)
-                        hipLaunchKernelGGL((k_encode_fixed_tile<16>), dim3((unsigned)full), dim3(kBlock),
-                                           (size_t)s->fix_tile_lds, st, pdw, S, out, status, stv);
-                    if (rem) {  // partial last tile: the lane-invariant dword kernel on the remainder
-                        const uint64_t b0 = full * s->fix_T;
-                        EncCols et = ec;
-                        for (const FixCol& fc : s->fcols) et.data[fc.col] = ec.data[fc.col] + b0 * fc.width;
-                        hipLaunchKernelGGL((k_encode_fixed_dw<true>), dim3(1), dim3(kBlock), lds_dw, st, pdw, et,
-                                           out + b0 * B, rem, status ? status + b0 : nullptr, stv);
-                    }
-                    break;
+            if (variant == 2) {
+                hipLaunchKernelGGL(k_encode_fixed_dw, dim3((unsigned)tiles), dim3(kBlock), lds_dw, st, pdw, ec, out,
+                                   (uint64_t)n, status, stv);
+            } else if (variant == 13) {
+                FixStage S;
+                memset(&S, 0, sizeof(S));
+                S.n = (int32_t)s->fcols.size();
+                for (int k = 0; k < S.n; k++) {
+                    const FixCol& fc = s->fcols[k];
+                    S.c[k] = FixStageCol{ec.data[fc.col], fc.width, fc.lds_off, fc.chunk_begin, fc.flags};
+                    S.flags |= (int32_t)(fc.flags & 1u);
                 }
-                default: variant = 8; break;
-            }
-            if (variant == 8) {
+                const uint64_t full = n / s->fix_T, rem = n - full * s->fix_T;
+                if (full)
+                    hipLaunchKernelGGL((k_encode_fixed_tile<16>), dim3((unsigned)full), dim3(kBlock),
+                                       (size_t)s->fix_tile_lds, st, pdw, S, out, status, stv);
+                if (rem) {  // partial last tile: the lane-invariant dword kernel on the remainder
+                    const uint64_t b0 = full * s->fix_T;
+                    EncCols et = ec;
+                    for (const FixCol& fc : s->fcols) et.data[fc.col] = ec.data[fc.col] + b0 * fc.width;
+                    hipLaunchKernelGGL(k_encode_fixed_dw, dim3(1), dim3(kBlock), lds_dw, st, pdw, et,
+                                       out + b0 * B, rem, status ? status + b0 : nullptr, stv);
+                }
+            } else {
                 hipLaunchKernelGGL(k_encode_fixed, dim3((unsigned)tiles), dim3(kBlock), gen_tables + fcb, st, pgen, ec,
                                    out, (uint64_t)n, status, stv);
             }
@@ -2266,129 +1396,47 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
                              : "out_offsets required for a variable-size schema");
         return PACKOS_E_INVALID;
     }
-    // default: size pass (k_sizes_affine or the k_stream_sizes look-back scan;
-    // skipped when the caller's offsets are ready) + k_encode_stream.  PACKOS_VAR_KERNEL=tile selects the
-    // two-kernel tiled encoder below.
-    const char* vk = getenv("PACKOS_VAR_KERNEL");
-    const bool want_stream = !(flags & PACKOS_ENC_FORCE_GENERIC) && !(vk && strcmp(vk, "tile") == 0);
-    S2Plan SP;
-    if (want_stream && s->conts.size() <= 64 && stream_plan(s, ec, SP)) {
-        if (!offs_ready) {
+    // default: k_encode_tiles.  Data-independent presence: the kernel computes
+    // (and writes) the out offsets itself, no size pass; otherwise the size pass
+    // (or the caller's PACKOS_ENC_OFFSETS_READY offsets) first, loaded per tile.
+    VPlan V;
+    const bool affine = !offs_ready && affine_layout(s, ec, nullptr);
+    if (!(flags & PACKOS_ENC_FORCE_GENERIC) && var_plan(s, ec, !affine, V)) {
+        if (!affine && !offs_ready) {
             if ((r = size_pass(s, t, ec, n, out_offsets, ws, ws_bytes, st))) return r;
         }
-        const uint64_t ntiles = (n + kS2T - 1) / kS2T;
-        static unsigned long long* sprof = nullptr;  // debug: PACKOS_STREAM_PROF=1 prints phase clocks
-        const bool want_prof = getenv("PACKOS_STREAM_PROF") != nullptr;
-        if (want_prof && !sprof) HIP_TRY(hipMalloc(&sprof, 16 * sizeof(unsigned long long)));
-        if (want_prof) HIP_TRY(hipMemsetAsync(sprof, 0, 16 * sizeof(unsigned long long), st));
-        SP.prof = want_prof ? sprof : nullptr;
-        hipLaunchKernelGGL(k_encode_stream, dim3((unsigned)ntiles), dim3(kBlock), SP.lds_total, st, t->enc, ec, SP,
-                           (const uint64_t*)out_offsets, out, cap, (uint64_t)n, status);
+        V.lits = t->enc.lits;
+        if (V.oseg >= 0) V.seg[V.oseg].src = (const uint8_t*)out_offsets;
+        const uint64_t ntiles = (n + kVT - 1) / kVT;
+#ifdef PACKOS_PHASE_PROF
+        static unsigned long long* prof[64] = {};
+        if (!prof[dev]) HIP_TRY(hipMalloc(&prof[dev], 8 * sizeof(unsigned long long)));
+        HIP_TRY(hipMemsetAsync(prof[dev], 0, 8 * sizeof(unsigned long long), st));
+        V.prof = prof[dev];
+#endif
+        if (V.aff)
+            hipLaunchKernelGGL(k_encode_tiles<true>, dim3((unsigned)ntiles), dim3(kVNT), V.lds_total, st, V,
+                               out_offsets, out, cap, (uint64_t)n, status);
+        else
+            hipLaunchKernelGGL(k_encode_tiles<false>, dim3((unsigned)ntiles), dim3(kVNT), V.lds_total, st, V,
+                               out_offsets, out, cap, (uint64_t)n, status);
         HIP_TRY(hipGetLastError());
-        if (want_prof) {
-            unsigned long long h[16];
-            HIP_TRY(hipMemcpyAsync(h, sprof, sizeof(h), hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
-            fprintf(stderr, "stream lds=%u img=%u holes=%u segs=%d vars=%d mid=%u tiles=%llu clocks/tile:",
-                    SP.lds_total, SP.img_bytes, SP.hole_cap, SP.nseg, SP.nvar, SP.mid, (unsigned long long)ntiles);
-            for (int i = 0; i < 8; i++) fprintf(stderr, " p%d=%.0f", i, (double)h[i] / ntiles);
-            fprintf(stderr, "\n");
-        }
+#ifdef PACKOS_PHASE_PROF
+        unsigned long long h[8];
+        HIP_TRY(hipMemcpyAsync(h, prof[dev], sizeof(h), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        fprintf(stderr, "k_encode_tiles lds=%u tiles=%llu clocks/tile: load=%.0f [round2=%.0f blobs=%.0f scan=%.0f] "
+                "frame=%.0f [chunks1=%.0f chunks2=%.0f]\n",
+                V.lds_total, (unsigned long long)ntiles, (double)h[0] / ntiles, (double)h[4] / ntiles,
+                (double)h[5] / ntiles, (double)h[1] / ntiles, (double)h[2] / ntiles, (double)h[6] / ntiles,
+                (double)h[3] / ntiles);
+#endif
         return PACKOS_OK;
     }
     if (!offs_ready) {
         if ((r = size_pass(s, t, ec, n, out_offsets, ws, ws_bytes, st))) return r;
     }
     const size_t npos = s->items.size() + 1;
-    int vt = 128;
-    uint32_t bud = 16384, in_bud = 16384;
-    if (const char* e = getenv("PACKOS_VAR_TILE")) vt = atoi(e);
-    if (const char* e = getenv("PACKOS_VAR_BUD")) bud = (uint32_t)std::max(2048, std::min(32768, atoi(e)));
-    if (const char* e = getenv("PACKOS_VAR_IN")) in_bud = (uint32_t)std::max(0, std::min(32768, atoi(e)));
-    if (vt != 64 && vt != 256) vt = 128;
-    uint32_t win_shift = 0;
-    while ((2u << win_shift) <= bud / 2) win_shift++;
-    // per-call plan: fixed regions (IT_FIXED items), var leaves, validity columns
-    VarPlan vp;
-    memset(&vp, 0, sizeof(vp));
-    for (int c = 0; c < kMaxCols; c++) vp.col_val[c] = -1;
-    bool plan_ok = !(flags & PACKOS_ENC_FORCE_GENERIC) && s->conts.size() <= 64 && s->items.size() < 255;
-    for (size_t c = 0; c < s->col_node.size() && plan_ok; c++) {
-        if (!ec.valid[c]) continue;
-        if (vp.nval >= kVPVal) { plan_ok = false; break; }
-        vp.col_val[c] = (int8_t)vp.nval;
-        vp.val_ptr[vp.nval++] = ec.valid[c];
-    }
-    auto plan_for = [&](int tile) {
-        vp.nfix = vp.nvar = 0;
-        uint32_t fb = 0;
-        for (size_t k = 0; k < s->items.size() && plan_ok; k++) {
-            const EncItem& it = s->items[k];
-            if (it.type == IT_FIXED) {
-                if (vp.nfix >= kVPFix) { plan_ok = false; break; }
-                vp.fix_ptr[vp.nfix] = ec.data[it.col];
-                vp.fix_w[vp.nfix] = it.size;
-                vp.fix_lds[vp.nfix] = fb;
-                fb += ((uint32_t)tile * it.size + 16 + 15) & ~15u;
-                vp.nfix++;
-            } else if (it.type == IT_VAR) {
-                if (vp.nvar >= kVPVar) { plan_ok = false; break; }
-                vp.var_off[vp.nvar] = ec.off[it.col];
-                vp.var_data[vp.nvar] = ec.data[it.col];
-                vp.var_item[vp.nvar] = (int)k;
-                vp.nvar++;
-            }
-        }
-        vp.fix_bytes = (int32_t)fb;
-        return fb;
-    };
-    VtLayout vl{};
-    uint32_t fb = 0;
-    for (;;) {
-        fb = plan_for(vt);
-        const uint32_t ib = std::max(in_bud, fb);  // fixed regions are always staged
-        vl = vt_layout(vt, t->enc, vp.nvar, vp.nval, bud, ib);
-        if ((vl.total <= 64 * 1024 && fb <= 32768) || vt == 64) break;
-        vt /= 2;
-    }
-    in_bud = std::max(in_bud, fb);
-    const bool tiled = plan_ok && vl.total <= 64 * 1024 && npos * 4 * kWavesPerBlock <= (size_t)bud &&
-                       ws && ws_bytes >= packos_encode_workspace_size(s, n);
-    if (tiled) {
-        uint8_t* wsb = (uint8_t*)ws + ((ws_scan_bytes(n) + 255) & ~(size_t)255);
-        uint32_t* tflags = (uint32_t*)wsb;
-        uint16_t* vpos = (uint16_t*)(wsb + ((ws_flag_bytes(n) + 255) & ~(size_t)255));
-        const dim3 g((unsigned)((n + vt - 1) / vt)), b(kBlock);
-        const size_t l = vl.total;
-        const uint64_t* o = out_offsets;
-        static unsigned long long* prof = nullptr;  // debug: PACKOS_VAR_PROF=1 prints phase cycles
-        const bool want_prof = getenv("PACKOS_VAR_PROF") != nullptr;
-        if (want_prof && !prof) HIP_TRY(hipMalloc(&prof, 16 * sizeof(unsigned long long)));
-        if (want_prof) HIP_TRY(hipMemsetAsync(prof, 0, 16 * sizeof(unsigned long long), st));
-        unsigned long long* pp = want_prof ? prof : nullptr;
-        if (vt == 64)
-            hipLaunchKernelGGL(k_encode_var_tile<64>, g, b, l, st, t->enc, ec, vp, o, out, cap, (uint64_t)n, status, bud, win_shift, in_bud, tflags, vpos, pp);
-        else if (vt == 128)
-            hipLaunchKernelGGL(k_encode_var_tile<128>, g, b, l, st, t->enc, ec, vp, o, out, cap, (uint64_t)n, status, bud, win_shift, in_bud, tflags, vpos, pp);
-        else
-            hipLaunchKernelGGL(k_encode_var_tile<256>, g, b, l, st, t->enc, ec, vp, o, out, cap, (uint64_t)n, status, bud, win_shift, in_bud, tflags, vpos, pp);
-        HIP_TRY(hipGetLastError());
-        if (vp.nvar > 0) {
-            if (vt == 64) hipLaunchKernelGGL(k_var_copy<64>, g, b, 0, st, vp, o, tflags, vpos, out, (uint64_t)n);
-            else if (vt == 128) hipLaunchKernelGGL(k_var_copy<128>, g, b, 0, st, vp, o, tflags, vpos, out, (uint64_t)n);
-            else hipLaunchKernelGGL(k_var_copy<256>, g, b, 0, st, vp, o, tflags, vpos, out, (uint64_t)n);
-            HIP_TRY(hipGetLastError());
-        }
-        if (want_prof) {
-            unsigned long long h[16];
-            HIP_TRY(hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
-            fprintf(stderr, "var_tile vt=%d lds=%zu blocks=%u ticks/block:", vt, l, g.x);
-            for (int i = 0; i < 8; i++) fprintf(stderr, " p%d=%.0f", i, (double)h[i] / g.x);
-            fprintf(stderr, "\n");
-        }
-        return PACKOS_OK;
-    }
     const size_t lds = (size_t)kWavesPerBlock * (kSlot + ((npos * 4 + 15) / 16) * 16);
     if (lds > 64 * 1024) { set_error("schema has too many items for the LDS budget"); return PACKOS_E_UNSUPPORTED; }
     const unsigned grid = (unsigned)std::min<uint64_t>((n + kWavesPerBlock - 1) / kWavesPerBlock, 256 * 16);
@@ -2430,7 +1478,7 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
     hipStream_t st = (hipStream_t)stream;
     const int64_t B = s->all_present_size;
     bool fast = s->dec_fast == 1 && ((uintptr_t)arena & 15) == 0 && (offsets || stride == (uint64_t)B) &&
-                !getenv("PACKOS_DECODE_GENERIC");
+                !s->tune.decode_generic;
     for (const DecFix& f : s->dfix) fast = fast && ((uintptr_t)dc.data[f.col] & 15) == 0;
     fast = fast && s->dfix.size() <= (size_t)kDecK;
     if (fast) {
@@ -2440,7 +1488,7 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
         // best for B >= 128 (M 0.111 -> 0.103 ms, C4 0.431 -> 0.409 ms); for
         // small blobs the larger tile loses more to fewer workgroups (C2 +7 %)
         int64_t tb = B >= 128 ? kDecTileBytesLarge : kDecTileBytes;
-        if (const char* e = getenv("PACKOS_DEC_TILE_BYTES")) tb = std::min<int64_t>(49152, std::max<int64_t>(1024, atoll(e)));
+        if (s->tune.dec_tile_bytes) tb = s->tune.dec_tile_bytes;
         F.T = (int32_t)std::min<int64_t>(1024, std::max<int64_t>(16, (tb / B) / 16 * 16));
         const uint32_t T = (uint32_t)F.T, QW = (uint32_t)((B + 3) / 4);
         const size_t lds = (size_t)T * B + 16 + 12 * QW + 4 * ((T + 1) & ~1u);
@@ -2457,9 +1505,6 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
         }
         hipLaunchKernelGGL(k_decode_fixed, dim3((unsigned)((n + T - 1) / T)), dim3(kBlock), lds, st, F, t->dec,
                            dc, K, arena, offsets, (uint64_t)n, status);
-    } else if (getenv("PACKOS_DECODE_NOWIN")) {
-        hipLaunchKernelGGL(k_decode, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, t->dec, dc,
-                           arena, offsets, stride, (uint64_t)n, status);
     } else {
         const size_t ptab = ((s->dnodes.size() * sizeof(DecNode) + 15) & ~(size_t)15) +
                             ((s->dkids.size() * 4 + 15) & ~(size_t)15) + s->lits.size() + 16;
@@ -2470,11 +1515,19 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
     return PACKOS_OK;
 }
 
-int packos_get_field_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride, size_t n,
-                           const int32_t* path, int depth, int want_tag, int want_width, uint64_t* out_start,
-                           uint32_t* out_len, uint8_t* out_tag, uint8_t* status, void* stream) {
+int packos_get_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride, size_t n, const int32_t* path,
+                     int depth, int getter, int want_tag, int want_width, uint8_t* out_values, uint32_t value_width,
+                     uint64_t* out_start, uint32_t* out_len, uint8_t* out_tag, uint8_t* status, void* stream) {
     if (!path || depth < 1 || depth > 16 || !out_start || !out_len || !out_tag || !status || (!arena && n))
         return PACKOS_E_INVALID;
+    if (getter < PACKOS_GET_FIXED || getter > PACKOS_GET_FLOAT) {
+        set_error("unknown getter");
+        return PACKOS_E_INVALID;
+    }
+    if (out_values && value_width == 0) {
+        set_error("out_values needs value_width > 0");
+        return PACKOS_E_INVALID;
+    }
     if (n == 0) return PACKOS_OK;
     if (!offsets && stride == 0) return PACKOS_E_INVALID;
     int dev, r;
@@ -2485,10 +1538,19 @@ int packos_get_field_batch(const uint8_t* arena, const uint64_t* offsets, uint64
         pa.p[d] = path[d];
     }
     hipLaunchKernelGGL(k_get_field, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                       (hipStream_t)stream, arena, offsets, stride, (uint64_t)n, pa, depth, want_tag, want_width,
-                       out_start, out_len, out_tag, status);
+                       (hipStream_t)stream, arena, offsets, stride, (uint64_t)n, pa, depth, getter, want_tag,
+                       want_width, out_values, value_width, out_start, out_len, out_tag, status);
     HIP_TRY(hipGetLastError());
     return PACKOS_OK;
+}
+
+// Exact-width (want_width >= 0) or span (want_width < 0) getter without a
+// typed gather: the round-1 entry point, kept for callers that bind it.
+int packos_get_field_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride, size_t n,
+                           const int32_t* path, int depth, int want_tag, int want_width, uint64_t* out_start,
+                           uint32_t* out_len, uint8_t* out_tag, uint8_t* status, void* stream) {
+    return packos_get_batch(arena, offsets, stride, n, path, depth, want_width >= 0 ? PACKOS_GET_FIXED : PACKOS_GET_SPAN,
+                            want_tag, want_width, nullptr, 0, out_start, out_len, out_tag, status, stream);
 }
 
 }  // extern "C"

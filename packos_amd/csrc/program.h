@@ -167,14 +167,13 @@ struct DecFix {
     uint32_t blob_off;     // first payload byte of the leaf inside the blob
     uint32_t flags;        // bit0: bool (normalise to 0/1)
     uint32_t magic;        // ceil(2^32 / width) for width > 1 (division by width)
-    uint32_t unit_begin;   // first 16-B output unit of this column in a full tile
-    uint32_t pad[2];
+    uint32_t pad[3];
 };
 
 struct DecFixProgram {
     const DecFix* cols;
     const uint32_t* chk;   // n_chk triples {blob dword q, constant-byte mask, constant value}, mask != 0
-    int32_t B, T, n_cols, total_units;
+    int32_t B, T, n_cols, pad;
     uint32_t q_magic;      // B % 4 == 0: ceil(2^32 / (B/4)) (0 when B/4 == 1)
     uint32_t b_magic;      // B % 4 != 0: ceil(2^32 / B)
     int32_t n_all_cols;    // every schema column (validity marking)
@@ -184,8 +183,9 @@ struct DecFixProgram {
 // column pointer tables passed by value as kernel arguments
 struct EncCols {
     const uint8_t* data[kMaxCols];
-    const uint32_t* off[kMaxCols];
+    const void* off[kMaxCols];      // var offsets: uint32_t[n+1], or uint64_t[n+1] when off64 bit c is set
     const uint8_t* valid[kMaxCols];
+    uint64_t off64;
 };
 
 struct DecCols {

@@ -1,5 +1,6 @@
 // schema_impl.h — host representation of a compiled schema (packos_schema).
 #pragma once
+#include <deque>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -22,6 +23,19 @@ struct Node {
     int parent = -1;
     int depth = 0;
     int top = -1;
+};
+
+// Tuning / testing knobs, read ONCE when the schema is compiled (never on the
+// launch path): PACKOS_VAR_PER (var staging pool bytes per blob of the
+// variable-size encoder), PACKOS_SIZES_SCAN=1 (look-back size kernel even for
+// closed-form layouts), PACKOS_DECODE_GENERIC=1 (thread-per-blob decoder even
+// for fixed layouts), PACKOS_DEC_TILE_BYTES (staged bytes per fixed-decode
+// tile), PACKOS_TILE_BYTES (fixed-encode tile bytes).
+struct Tune {
+    int var_per = 40;
+    bool sizes_scan = false;
+    bool decode_generic = false;
+    int dec_tile_bytes = 0;      // 0: 24 KB for B >= 128, else 16 KB
 };
 
 struct DeviceTables {
@@ -74,18 +88,20 @@ struct packos_schema {
     std::vector<packos::DecFix> dfix;
     std::vector<uint32_t> dchk;
     std::vector<uint8_t> canon;       // all-present blob, zero payload bytes
-    int dfix_units = 0;
     int dec_fast = 0;                 // 1: canonical blob decodes (set at compile)
+
+    packos::Tune tune;
 
     std::string describe;
 
     std::mutex mu;
-    std::vector<packos::DeviceTables> dev;
+    std::deque<packos::DeviceTables> dev;   // deque: pointers handed out stay valid
 };
 
 namespace packos {
 // thread-local last error string
 void set_error(const std::string& m);
+void read_tune(Tune& t);
 int upload_tables(packos_schema* s, int device, DeviceTables** out);
 // host run of the device decoder over the canonical blob (kernels.hip)
 bool canonical_decodes(const packos_schema* s);

@@ -21,7 +21,7 @@ MODE_PACKABLE = 1
 
 class PackosColumn(C.Structure):
     _fields_ = [("data", C.c_void_p), ("offsets", C.c_void_p), ("valid", C.c_void_p),
-                ("start", C.c_void_p), ("length", C.c_void_p)]
+                ("start", C.c_void_p), ("length", C.c_void_p), ("offsets64", C.c_void_p)]
 
 
 class OrSchema(C.Structure):
@@ -81,6 +81,9 @@ def lib():
         L.or_get_field_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_size_t,
                                          C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                          C.c_void_p, C.c_void_p, C.c_void_p]
+        L.or_get_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_size_t, C.c_void_p,
+                                   C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_uint32,
+                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -227,6 +230,26 @@ def get_field_batch(arena, offsets, n, path, want_tag, want_width, stride=0):
     lib().or_get_field_batch(_ptr(a), _ptr(o), stride, n, _ptr(p), len(path), want_tag,
                              want_width, _ptr(s0), _ptr(ln), _ptr(tg), _ptr(st))
     return s0[:n], ln[:n], tg[:n], st[:n]
+
+
+def get_batch(arena, offsets, n, path, getter, want_tag=0, want_width=0, stride=0, values=True):
+    """or_get_batch: (values, start, length, tag, status), same contract as
+    packos_amd.api.get_batch."""
+    a = np.ascontiguousarray(arena, dtype=np.uint8)
+    if a.size == 0:
+        a = np.zeros(1, np.uint8)
+    o = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+    p = np.asarray(path, dtype=np.int32)
+    vw = 8 if getter in (3, 4) else max(want_width, 0)
+    gather = values and getter != 2 and vw > 0
+    vals = np.zeros((max(n, 1), vw), np.uint8) if gather else None
+    s0 = np.zeros(max(n, 1), np.uint64)
+    ln = np.zeros(max(n, 1), np.uint32)
+    tg = np.zeros(max(n, 1), np.uint8)
+    st = np.zeros(max(n, 1), np.uint8)
+    lib().or_get_batch(_ptr(a), _ptr(o), stride, n, _ptr(p), len(path), getter, want_tag, want_width,
+                       _ptr(vals), vw if gather else 0, _ptr(s0), _ptr(ln), _ptr(tg), _ptr(st))
+    return (None if vals is None else vals[:n]), s0[:n], ln[:n], tg[:n], st[:n]
 
 
 # ---- single-buffer GetAccess / SeqGetAccess wrappers (golden decode tests) ----

@@ -4,13 +4,15 @@ Every test calls libpackos.so through the C ABI on cuda:0 and compares with
 the oracle on the same seeded inputs (oracle pinned by test_oracle_golden.py)
 or with the reference's golden bytes directly.
 """
+import ctypes as C
+
 import numpy as np
 import pytest
 
 import oracle_bridge as ob
 from packos_amd import _lib
 from golden_util import MODES, chain_of, load, unwrap
-from packos_amd.api import CompiledSchema, DeviceColumns, decode_batch, encode_batch, get_field_batch
+from packos_amd.api import CompiledSchema, DeviceColumns, decode_batch, encode_batch, get_batch, get_field_batch
 from packos_amd.columns import HostColumns
 from packos_amd.configs import CONFIGS, make_columns
 from packos_amd.schema import SBool, SChain, SInt16, SInt32, SInt64, SStringLen, SVariableString, STuple, SMap, SString
@@ -82,17 +84,20 @@ def test_golden_cross_api(case):
 
 
 # --------------------------------------------------------------- encode ----
-STREAM_KNOBS = [{}, {"PACKOS_STREAM_IMG": "4096"}, {"PACKOS_STREAM_LONG": "32"}, {"PACKOS_STREAM_LONG": "200"},
-                {"PACKOS_STREAM_IMG": "6000", "PACKOS_STREAM_LONG": "32"}, {"PACKOS_STREAM_VAR": "0"},
-                {"PACKOS_STREAM_FIX": "0"}, {"PACKOS_STREAM_MID": "0"}, {"PACKOS_STREAM_MID": "1"},
-                {"PACKOS_STREAM_MID": "99"}, {"PACKOS_STREAM_VAR": "600", "PACKOS_STREAM_FIX": "300"}]
+# k_encode_tiles knobs (read when the schema compiles): PACKOS_VAR_PER = var
+# staging pool bytes per blob (0: no var column is ever staged -> every value
+# > 16 B is a hole, shorter ones take the HBM slow path; 8: tiles stage some
+# columns and not others; 256: everything staged), PACKOS_SIZES_SCAN = the
+# look-back size pass + loaded offsets instead of the closed form
+VAR_KNOBS = [{}, {"PACKOS_VAR_PER": "0"}, {"PACKOS_VAR_PER": "8"}, {"PACKOS_VAR_PER": "256"},
+             {"PACKOS_SIZES_SCAN": "1"}, {"PACKOS_SIZES_SCAN": "1", "PACKOS_VAR_PER": "0"}]
 
 
 @pytest.mark.parametrize("fused", [False, True], ids=["offsets_ready", "single_pass"])
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("seed", range(60))
 def test_random_schema_encode(seed, mode, fused):
-    # default var path: k_encode_stream (caller offsets, or its own look-back scan)
+    # default var path: k_encode_tiles (caller offsets, or its own layout)
     chain = rand_chain(seed)
     hc = HostColumns.from_rows(chain, rand_rows(chain, 257 + 300 * (seed % 3), seed * 7 + 1))
     assert_same_encoding(chain, hc, mode, f"seed {seed}", fused=fused)
@@ -129,9 +134,9 @@ def test_size_pass_var_base_and_counts(n, seed, scan, monkeypatch):
     assert np.array_equal(r.status.cpu().numpy().astype(np.uint32), s0)
 
 
-@pytest.mark.parametrize("knobs", STREAM_KNOBS[1:], ids=lambda k: ",".join(f"{a[14:]}={b}" for a, b in k.items()))
+@pytest.mark.parametrize("knobs", VAR_KNOBS[1:], ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()))
 @pytest.mark.parametrize("seed", range(0, 60, 6))
-def test_random_schema_encode_stream_knobs(seed, knobs, monkeypatch):
+def test_random_schema_encode_var_knobs(seed, knobs, monkeypatch):
     for k, v in knobs.items():
         monkeypatch.setenv(k, v)
     chain = rand_chain(seed)
@@ -142,8 +147,8 @@ def test_random_schema_encode_stream_knobs(seed, knobs, monkeypatch):
 @pytest.mark.parametrize("fields,tuples,nest", [(43, 0, 0), (44, 0, 0), (45, 0, 0), (60, 0, 0), (6, 15, 0),
                                                (6, 16, 0), (6, 0, 12)])
 def test_stream_plan_limits(fields, tuples, nest):
-    """Schemas at and past the stream encoder's plan limits (48 items, 16
-    containers): past them the call routes to the tiled encoder; both must
+    """Schemas at and past the tile encoder's plan limits (48 items, 16
+    containers): past them the call routes to k_encode_var; both must
     match the oracle.  Items = one header block per container + the leaves:
     `fields` flat leaves, `tuples` one-leaf tuples (one container each), and a
     tuple nested `nest` deep (12 is the compiler's depth limit)."""
@@ -204,27 +209,17 @@ def test_encode_host_batch_random(seed):
         assert np.array_equal(o0, o1) and np.array_equal(a0, a1) and np.array_equal(s0, s1.astype(np.uint32))
 
 
-@pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("seed", range(20))
-def test_random_schema_encode_tile_kernel(seed, mode, monkeypatch):
-    # PACKOS_VAR_KERNEL=tile: the two-kernel tiled encoder (size pass + tile kernel)
-    monkeypatch.setenv("PACKOS_VAR_KERNEL", "tile")
-    chain = rand_chain(seed)
-    hc = HostColumns.from_rows(chain, rand_rows(chain, 257, seed * 7 + 1))
-    assert_same_encoding(chain, hc, mode, f"tile seed {seed}")
-
-
 @pytest.mark.parametrize("fused", [False, True], ids=["offsets_ready", "single_pass"])
-@pytest.mark.parametrize("knobs", STREAM_KNOBS, ids=lambda k: ",".join(f"{a[14:]}={b}" for a, b in k.items()) or "default")
-def test_stream_long_values_and_budgets(knobs, fused, monkeypatch):
-    """k_encode_stream: values around the long-value threshold at every 16-B
-    alignment (head / hole / tail split), adjacent long values, nil
-    containers; small image budgets that push tiles onto the per-blob
-    fallback, unstaged var / fixed columns (HBM reads), every emitter split."""
+@pytest.mark.parametrize("knobs", VAR_KNOBS, ids=lambda k: ",".join(f"{a[7:]}={b}" for a, b in k.items()) or "default")
+def test_var_holes_and_budgets(knobs, fused, monkeypatch):
+    """k_encode_tiles: values around the 16-B hole threshold at every 16-B
+    alignment (a chunk = tail of one hole + frame bytes + head of the next),
+    adjacent long values, nil containers, staged / unstaged var columns, the
+    HBM slow path for short unstaged values."""
     for k, v in knobs.items():
         monkeypatch.setenv(k, v)
-    img = knobs.get("PACKOS_STREAM_IMG")
-    longv = knobs.get("PACKOS_STREAM_LONG")
+    img = knobs.get("PACKOS_VAR_PER")
+    longv = knobs.get("PACKOS_SIZES_SCAN")
     chain = SChain(SInt16, SVariableString(), SVariableString(), STuple(SVariableString(), SInt16),
                    SStringLen(100))
     rng = np.random.default_rng(11)
@@ -238,7 +233,7 @@ def test_stream_long_values_and_budgets(knobs, fused, monkeypatch):
                      None if rng.random() < 0.15 else ["t" * c, -i], "p" * 100])
     hc = HostColumns.from_rows(chain, rows)
     for mode in (0, 1):
-        assert_same_encoding(chain, hc, mode, f"stream img={img} longv={longv} mode={mode}", fused=fused)
+        assert_same_encoding(chain, hc, mode, f"var_per={img} scan={longv} mode={mode}", fused=fused)
 
 
 @pytest.mark.parametrize("mode", [0, 1])
@@ -251,11 +246,11 @@ def test_random_schema_encode_wave_kernel(seed, mode):
     assert_same_encoding(chain, hc, mode, f"wave seed {seed}", flags=_lib.ENC_FORCE_GENERIC)
 
 
-@pytest.mark.parametrize("kernel", ["stream", "stream_fused", "tile"])
+@pytest.mark.parametrize("kernel", ["tiles", "tiles_fused", "tiles_no_pool"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_var_tile_runs_and_fallbacks(mode, kernel, monkeypatch):
-    """Tiled var encode: runs split at 8 KiB windows, runs larger than the LDS
-    budget, blobs > 64 KiB (whole-tile fallback), and ragged last tiles."""
+    """Tiled var encode: long values (holes), blobs > 64 KiB (whole-tile
+    per-blob fallback), nil containers, and ragged last tiles."""
     chain = SChain(SInt16, SVariableString(), STuple(SVariableString(), SInt16))
     rng = np.random.default_rng(5)
     rows = []
@@ -264,9 +259,9 @@ def test_var_tile_runs_and_fallbacks(mode, kernel, monkeypatch):
         ln = int(rng.integers(0, 40)) if r < 0.7 else int(rng.integers(3000, 12000)) if r < 0.97 else 70_000
         rows.append([i, "s" * ln, None if rng.random() < 0.1 else ["t" * int(rng.integers(0, 300)), -i]])
     hc = HostColumns.from_rows(chain, rows)
-    if kernel == "tile":
-        monkeypatch.setenv("PACKOS_VAR_KERNEL", "tile")
-    assert_same_encoding(chain, hc, mode, f"tile edges {kernel}", fused=kernel == "stream_fused")
+    if kernel == "tiles_no_pool":
+        monkeypatch.setenv("PACKOS_VAR_PER", "0")
+    assert_same_encoding(chain, hc, mode, f"tile edges {kernel}", fused=kernel == "tiles_fused")
 
 
 def test_var_encode_capacity_overrun():
@@ -294,6 +289,91 @@ def test_var_encode_capacity_overrun():
     assert np.array_equal(out.cpu().numpy()[:last], a0[:last])
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("nil", [False, True])
+def test_var_wide_fixed_holes(mode, nil):
+    """Fixed leaves wider than 16 B in a var schema stay in HBM as holes
+    (copied by the chunk pass straight from their column rows), next to var
+    values, literals and nullable scalars."""
+    chain = SChain(SInt16, SVariableString(), SStringLen(40), STuple(SStringLen(17), SInt16), SStringLen(100),
+                   SMap(SString.Match("key"), SStringLen(33)), SInt32)
+    rng = np.random.default_rng(3 + mode + 2 * nil)
+    rows = []
+    for i in range(2100):
+        rows.append([i, "v" * int(rng.integers(0, 70)), "a" * 40,
+                     None if (nil and rng.random() < 0.2) else ["b" * 17, -i], "c" * 100,
+                     None if (nil and rng.random() < 0.2) else {"key": "d" * 33}, 7 * i])
+    hc = HostColumns.from_rows(chain, rows)
+    assert_same_encoding(chain, hc, mode, f"wide fixed holes mode={mode} nil={nil}")
+    assert_same_encoding(chain, hc, mode, f"wide fixed holes mode={mode} nil={nil} fused", fused=True)
+
+
+@pytest.mark.parametrize("shift", [1, 3, 7, 8, 13])
+def test_var_unaligned_columns(shift):
+    """Column data at arbitrary byte alignment (views at an offset): every
+    staged row array and every hole source is misaligned differently."""
+    T = torch()
+    cfg = CONFIGS["C3"]
+    hc = make_columns(cfg, n=3001)
+    s = CompiledSchema(cfg.chain, cfg.mode)
+    dc = DeviceColumns.from_host(s, hc, "cuda:0")
+    for c, d in enumerate(dc.data):
+        if d is not None:
+            k = shift + 2 * c
+            buf = T.zeros(d.numel() + 64, dtype=T.uint8, device="cuda:0")
+            buf[k:k + d.numel()] = d
+            dc.data[c] = buf[k:k + d.numel()]
+    r = encode_batch(s, dc)
+    T.cuda.synchronize()
+    a0, o0, s0 = ob.encode(cfg.chain, hc, cfg.mode, nthreads=8)
+    assert np.array_equal(r.offsets.cpu().numpy().astype(np.uint64), o0)
+    assert np.array_equal(r.arena[: r.total].cpu().numpy(), a0)
+
+
+@pytest.mark.parametrize("base_gib", [0, 4.25])
+def test_var_offsets64(base_gib):
+    """64-bit var offsets (packos_column.offsets64): the C5 schema with its var
+    arenas placed `base_gib` GiB into one device allocation, so the offsets
+    have high bits set; bytes and offsets equal the oracle's (which reads the
+    same values through 32-bit offsets relative to the arena start)."""
+    T = torch()
+    cfg = CONFIGS["C5"]
+    n = 4099
+    hc = make_columns(cfg, n=n)
+    s = CompiledSchema(cfg.chain, cfg.mode)
+    dc = DeviceColumns.from_host(s, hc, "cuda:0")
+    base = int(base_gib * 2 ** 30)
+    var_cols = [c for c, o in enumerate(dc.offsets) if o is not None]
+    total_var = sum(int(hc.offsets[c][-1]) for c in var_cols)
+    big = T.empty(base + total_var + 64, dtype=T.uint8, device="cuda:0")
+    arr = dc.ctypes_array()
+    keep = []
+    pos = base
+    for c in var_cols:
+        ln = int(hc.offsets[c][-1])
+        big[pos:pos + ln] = dc.data[c][:ln]
+        o64 = T.from_numpy(hc.offsets[c].astype(np.int64) + pos).to("cuda:0")
+        keep.append(o64)
+        arr[c].data = big.data_ptr()
+        arr[c].offsets = None
+        arr[c].offsets64 = o64.data_ptr()
+        pos += ln
+    L = _lib.lib()
+    a0, o0, s0 = ob.encode(cfg.chain, hc, cfg.mode, nthreads=8)
+    out = T.zeros(int(o0[n]) + 16, dtype=T.uint8, device="cuda:0")
+    offs = T.empty(n + 1, dtype=T.int64, device="cuda:0")
+    st = T.empty(n, dtype=T.int32, device="cuda:0")
+    wsb = L.packos_encode_workspace_size(s.handle, n)
+    ws = T.empty(max(wsb, 16), dtype=T.uint8, device="cuda:0")
+    for flags in (0, _lib.ENC_FORCE_GENERIC):
+        assert L.packos_encode_batch(s.handle, arr, n, out.data_ptr(), out.numel(), offs.data_ptr(), st.data_ptr(),
+                                     ws.data_ptr(), wsb, flags, None) == 0, L.packos_last_error()
+        T.cuda.synchronize()
+        assert np.array_equal(offs.cpu().numpy().astype(np.uint64), o0)
+        assert np.array_equal(out[: int(o0[n])].cpu().numpy(), a0)
+    del big
+
+
 @pytest.mark.parametrize("seed", range(30))
 def test_random_fixed_schema_encode(seed):
     # no var leaves, no nils: exercises the LDS-tiled fixed-layout kernel
@@ -303,7 +383,7 @@ def test_random_fixed_schema_encode(seed):
     assert_same_encoding(chain, hc, 0, f"fixed seed {seed}")
 
 
-@pytest.mark.parametrize("variant", [13, 2, 1, 8])
+@pytest.mark.parametrize("variant", [13, 2, 8])
 @pytest.mark.parametrize("seed", range(16))
 def test_fixed_kernel_variants(seed, variant):
     """Every fixed-layout kernel on random fixed schemas padded (one extra
@@ -373,13 +453,13 @@ def gpu_decode(chain, arena_np, offs_np, n, stride=0):
     return out, st.cpu().numpy().astype(np.uint32)
 
 
-def assert_same_decode(chain, arena, offs, n, what="", stride=0):
+def assert_same_decode(chain, arena, offs, n, what="", stride=0, gpu=None):
     """Statuses must match for every blob; leaf columns for every blob that
     decodes (status 0).  DecodeBuffer returns (nil, err) on failure
     (schema/schema.go:900-903), so a failing blob's columns are unspecified
     (the fixed-layout fast path may leave tile data in them)."""
     o_out, o_st = ob.decode(chain, arena, offs, n, nthreads=8)
-    g_out, g_st = gpu_decode(chain, arena, offs, n, stride)
+    g_out, g_st = gpu_decode(chain, arena, offs, n, stride) if gpu is None else gpu
     if not np.array_equal(o_st, g_st):
         bad = int(np.nonzero(o_st != g_st)[0][0])
         raise AssertionError(f"{what}: status blob {bad}: oracle {o_st[bad]:#x} gpu {g_st[bad]:#x}")
@@ -468,11 +548,73 @@ def test_random_decode_corrupted(seed):
     assert_same_decode(chain, arena2, np.asarray(noffs, np.uint64), n, f"corrupt seed {seed}")
 
 
+class _RawDevBuf:
+    """An exactly sized hipMalloc allocation (torch's caching allocator
+    rounds up to 2 MiB segments, hiding over-reads past an arena's end)."""
+
+    def __init__(self, data: np.ndarray):
+        T = torch()
+        self.hip = C.CDLL("libamdhip64.so")
+        self.size = (data.size + 4095) // 4096 * 4096
+        p = C.c_void_p()
+        assert self.hip.hipMalloc(C.byref(p), C.c_size_t(self.size)) == 0
+        self.base = p.value
+        self.ptr = self.base + self.size - data.size   # arena ends at the allocation's (page) end
+        assert self.hip.hipMemcpy(C.c_void_p(self.ptr), data.ctypes.data_as(C.c_void_p),
+                                  C.c_size_t(data.size), 1) == 0
+        self.device = T.device("cuda:0")
+
+    def data_ptr(self):
+        return self.ptr
+
+    def free(self):
+        self.hip.hipDeviceSynchronize()
+        self.hip.hipFree(C.c_void_p(self.base))
+
+
+@pytest.mark.parametrize("cfg,seed", [("M", 0), ("M", 1), ("C1", 2)])
+def test_decode_fixed_truncated_exact_alloc(cfg, seed):
+    """A fixed-schema batch whose blobs are truncated (end offsets pulled
+    inward) decoded from an arena that ends exactly at the end of its
+    allocation, on a page boundary: the fixed-layout tile staging must stop
+    at the tile's last offset, and statuses match the oracle."""
+    T = torch()
+    rng = np.random.default_rng(seed)
+    c = CONFIGS[cfg]
+    if CompiledSchema(c.chain, 0).fixed_blob_size <= 0:
+        pytest.skip("not a fixed schema")
+    n = 3000
+    hc = make_columns(c, n=n, seed=seed)
+    arena, offs, _ = ob.encode(c.chain, hc, 0, nthreads=8)
+    starts, ends = offs[:-1].astype(np.int64), offs[1:].astype(np.int64)
+    cut = rng.random(n) < 0.02
+    cut[-1] = True                                   # the last tile runs short too
+    ends_cut = np.where(cut, starts + (ends - starts) // 3, ends)
+    pieces, noffs = [], [0]
+    for i in range(n):
+        pieces.append(arena[starts[i]:ends_cut[i]])
+        noffs.append(noffs[-1] + int(ends_cut[i] - starts[i]))
+    pad = (-noffs[-1]) % 16                          # keep the arena base 16-B aligned
+    arena2 = np.concatenate(pieces + [np.zeros(0, np.uint8)])
+    buf = np.concatenate([np.zeros(pad, np.uint8), arena2])
+    noffs = np.asarray(noffs, np.uint64) + np.uint64(pad)
+    raw = _RawDevBuf(buf)
+    try:
+        s = CompiledSchema(c.chain, 0)
+        do = T.from_numpy(noffs.astype(np.int64)).to("cuda:0")
+        out, st = decode_batch(s, raw, do, n)
+        T.cuda.synchronize()
+        g = (out, st.cpu().numpy().astype(np.uint32))
+    finally:
+        raw.free()
+    got = assert_same_decode(c.chain, buf, noffs, n, f"truncated {cfg}", gpu=g)
+    assert (got[~cut] == 0).all()
+
+
 @pytest.mark.parametrize("seed", range(12))
-def test_decode_without_window(seed, monkeypatch):
-    """PACKOS_DECODE_NOWIN: the plain thread-per-blob decoder (no LDS window)
-    on clean and corrupted batches must agree with the oracle too."""
-    monkeypatch.setenv("PACKOS_DECODE_NOWIN", "1")
+def test_decode_generic_kernel(seed, monkeypatch):
+    """PACKOS_DECODE_GENERIC: the thread-per-blob decoder (k_decode_win) even
+    where the fixed-layout fast path applies, on clean and corrupted batches."""
     monkeypatch.setenv("PACKOS_DECODE_GENERIC", "1")
     rng = np.random.default_rng(77 + seed)
     chain = rand_chain(seed)
@@ -614,3 +756,69 @@ def test_random_get(seed):
         okm = o[3] == 0
         assert np.array_equal(o[0][okm], gs[0].astype(np.uint64)[okm])
         assert np.array_equal(o[1][okm], gs[1].astype(np.uint32)[okm])
+
+
+GETTERS = [(0, 1, 1), (0, 1, 2), (0, 1, 4), (0, 1, 8), (0, 3, 4), (0, 3, 8), (0, 5, 1),
+           (1, 1, 4), (1, 1, 8), (1, 3, 8), (1, 5, 1), (2, 6, 0), (2, 4, 0), (2, 7, 0),
+           (3, 0, 0), (4, 0, 0)]
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_get_batch(seed):
+    """packos_get_batch vs or_get_batch for every getter family (FIXED,
+    NULLABLE, SPAN, INT, FLOAT) with typed gather, on random schemas whose
+    nullable columns hold nils (width-0 fields) and a third of the blobs
+    corrupted."""
+    T = torch()
+    rng = np.random.default_rng(100 + seed)
+    chain = rand_chain(seed)
+    hc = HostColumns.from_rows(chain, rand_rows(chain, 300, seed))
+    arena, offs, _ = ob.encode(chain, hc, int(rng.integers(0, 2)))
+    arena = arena.copy()
+    for i in range(0, hc.n, 3):
+        a, b = int(offs[i]), int(offs[i + 1])
+        if b > a:
+            arena[a + int(rng.integers(0, min(8, b - a)))] = rng.integers(0, 256)
+    da = T.from_numpy(arena).to("cuda:0")
+    do = T.from_numpy(offs.astype(np.int64)).to("cuda:0")
+    for _ in range(10):
+        depth = int(rng.integers(1, 3))
+        path = [int(rng.integers(0, 6)) for _ in range(depth)]
+        getter, tag, width = GETTERS[int(rng.integers(0, len(GETTERS)))]
+        o = ob.get_batch(arena, offs, hc.n, path, getter, tag, width)
+        g = [None if x is None else x.cpu().numpy() for x in get_batch(da, do, hc.n, path, getter, tag, width)]
+        what = (path, getter, tag, width)
+        assert np.array_equal(o[4], g[4]), what
+        assert np.array_equal(o[3], g[3]), what
+        assert np.array_equal(o[1], g[1].astype(np.uint64)), what
+        assert np.array_equal(o[2], g[2].astype(np.uint32)), what
+        if o[0] is None:
+            assert g[0] is None
+        else:
+            assert np.array_equal(o[0], g[0]), what
+
+
+def test_get_batch_nullable_and_any_width():
+    """Hand-built blob with nil (width-0) fields: GetNullable* returns nil
+    before checking the tag, GetInt/GetFloating take any legal width."""
+    T = torch()
+    blob = _blob_with_nils()
+    buf = np.frombuffer(blob * 3, np.uint8).copy()
+    offs = np.arange(4, dtype=np.uint64) * len(blob)
+    da = T.from_numpy(buf).to("cuda:0")
+    for path, getter, tag, width in [([1], 1, 5, 1), ([1], 3, 0, 0), ([7], 3, 0, 0), ([2], 4, 0, 0),
+                                     ([5], 4, 0, 0), ([3], 0, 5, 1), ([6], 3, 0, 0), ([4], 2, 6, 0)]:
+        o = ob.get_batch(buf, offs, 3, path, getter, tag, width)
+        g = get_batch(da, None, 3, path, getter, tag, width, stride=len(blob))
+        T.cuda.synchronize()
+        assert np.array_equal(o[4], g[4].cpu().numpy())
+        if o[0] is not None:
+            assert np.array_equal(o[0], g[0].cpu().numpy())
+
+
+def _blob_with_nils():
+    from test_oracle_golden import pack_fields
+    return pack_fields(NIL_FIELDS)
+
+
+from test_oracle_golden import NIL_FIELDS  # noqa: E402

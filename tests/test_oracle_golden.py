@@ -66,6 +66,54 @@ def test_getaccess_wrong_type_and_width():
     assert ob.get_field_batch(buf, offs, 1, [0, 0], 6, -1)[3][0] == 1
 
 
+def pack_fields(fields):
+    """Lay fields [(tag, bytes)] out in the wire format (header block of
+    uint16 offset<<3|tag, End entry holding the payload length;
+    pack.go:9-60): h0 is absolute, later offsets relative to the payload."""
+    base = 2 * (len(fields) + 1)
+    hdr, pay = [], b""
+    for i, (tag, b) in enumerate(fields):
+        hdr.append(((base if i == 0 else len(pay)) << 3) | tag)
+        pay += b
+    hdr.append(len(pay) << 3)
+    return b"".join(h.to_bytes(2, "little") for h in hdr) + pay
+
+
+# Integer int16, nil Integer, Floating f32, Bool 7, String, nil Floating,
+# 3-byte Integer, Integer int8 -5
+NIL_FIELDS = [(1, (-300).to_bytes(2, "little", signed=True)), (1, b""), (3, bytes.fromhex("0000c03f")),
+              (5, b"\x07"), (6, b"abc"), (3, b""), (1, b"\x01\x02\x03"), (1, bytes([0xFB]))]
+
+
+@pytest.mark.parametrize("path,getter,tag,width,status,value", [
+    ([1], 1, 1, 4, 4, None),            # GetNullableInt32 on nil -> nil, no error
+    ([1], 1, 5, 1, 4, None),            # GetNullableBool on a nil Integer: nil before the tag check
+    ([1], 0, 1, 4, 1, None),            # GetInt32 on nil -> width error
+    ([0], 1, 1, 2, 0, "d4fe"),          # GetNullableInt16 on a value
+    ([0], 3, 0, 0, 0, "d4feffffffffffff"),  # GetInt -> int16 sign-extended
+    ([7], 3, 0, 0, 0, "fbffffffffffffff"),  # GetInt -> int8 -5
+    ([6], 3, 0, 0, 1, None),            # GetInt on a 3-byte integer -> error
+    ([1], 3, 0, 0, 4, None),            # GetInt on nil -> nil
+    ([2], 3, 0, 0, 1, None),            # GetInt on Floating -> tag error
+    ([2], 4, 0, 0, 0, "0000c03f00000000"),  # GetFloating -> float32 bits
+    ([5], 4, 0, 0, 4, None),            # GetFloating on nil -> nil
+    ([3], 0, 5, 1, 0, "01"),            # GetBool normalises to 0/1
+    ([3], 1, 5, 1, 0, "01"),            # GetNullableBool
+    ([4], 2, 6, 0, 0, None),            # GetString span
+    ([5], 2, 6, 0, 1, None),            # GetBytes on a Floating -> tag error
+    ([9], 1, 1, 4, 1, None),            # past argCount: TypeEnd, width -1 -> tag error
+])
+def test_get_batch_getters(path, getter, tag, width, status, value):
+    blob = pack_fields(NIL_FIELDS)
+    buf = np.frombuffer(blob, np.uint8)
+    vals, s0, ln, tg, st = ob.get_batch(buf, np.asarray([0, len(blob)], np.uint64), 1, path, getter, tag, width)
+    assert st[0] == status
+    if value is not None:
+        assert bytes(vals[0]).hex() == value
+    if getter == 2 and status == 0:
+        assert bytes(buf[int(s0[0]):int(s0[0]) + int(ln[0])]) == b"abc"
+
+
 def test_seqget_nested_map_golden():
     # access/seqget_test.go:11-101
     case = next(c for c in G["seq"] if c["id"] == "seq_nested_map")
