@@ -85,6 +85,10 @@ extern "C" {
  * bits 0..7   schema ErrorCode of the error DecodeBuffer/ValidateBuffer would
  *             return (schema/schema.go:24-41); 0 = ok
  * bits 8..23  top-level field position of that error + 1 (0 = position -1)
+ * bits 24..29 encode only: the ErrorCode of the leaf error that EncodeValue
+ *             wraps in ErrEncode (schema.go:919-936), e.g. ErrOutOfRange for
+ *             a Range violation; bits 0..7 then hold PACKOS_ERR_ENCODE and
+ *             bits 8..23 the top-level field that failed first
  * bit 30      the reference would panic (Go runtime index out of range) on
  *             this blob, e.g. a nullable int16 field of width 1
  * bit 31      encode: an offset >= 8192 was truncated to 13 bits exactly as
@@ -93,6 +97,7 @@ extern "C" {
  */
 #define PACKOS_STATUS_CODE(s)      ((int)((s) & 0xFFu))
 #define PACKOS_STATUS_POS(s)       ((int)(((s) >> 8) & 0xFFFFu) - 1)
+#define PACKOS_STATUS_INNER(s)     ((int)(((s) >> 24) & 0x3Fu))
 #define PACKOS_STATUS_PANIC        0x40000000u
 #define PACKOS_STATUS_OVERFLOW13   0x80000000u
 
@@ -101,8 +106,17 @@ extern "C" {
 #define PACKOS_ERR_UNEXPECTED_EOF        2
 #define PACKOS_ERR_CONSTRAINT_VIOLATED   3
 #define PACKOS_ERR_ENCODE                4
+#define PACKOS_ERR_STRING_PREFIX         6
+#define PACKOS_ERR_STRING_SUFFIX         7
 #define PACKOS_ERR_STRING_MATCH          9
 #define PACKOS_ERR_OUT_OF_RANGE         13
+#define PACKOS_ERR_DATE_OUT_OF_RANGE    14
+
+/* decode view of a string leaf with a decodeDefault whose payload was empty:
+ * start = PACKOS_VIEW_DEFAULT, length = the default's length; the bytes are
+ * the schema's literal (packos_schema_column_default), as the reference
+ * returns DefaultDecodeVal instead of "" (schema/schema.go:279-286)          */
+#define PACKOS_VIEW_DEFAULT  0x8000000000000000ull
 
 /* ---- columns ---------------------------------------------------------------
  * One packos_column per schema node in depth-first (pre-order) schema order:
@@ -157,7 +171,22 @@ typedef struct packos_schema packos_schema;
  * bytes (width), tuple (schema, fieldNames, nullable, variableLength),
  * map (schema = key,value,... ; keys with "exact" become constants;
  * "sorted": true sorts the pairs by key bytes at compile time, which is
- * PackMapSorted / AddMapSortedKey order).                                    */
+ * PackMapSorted / AddMapSortedKey order).
+ * Value checks, as BuildSchema builds them:
+ *   int16/32/64 "min"/"max"   -> SInt*.Range: never nullable, ErrOutOfRange
+ *                                (schema.go:1172-1364); int8 ignores them
+ *   "date" (dateFrom/dateTo   -> SDateRange: int64 payload, nullable per
+ *   RFC3339, both or neither)    "nullable", ErrDateOutOfRange (:2188-2250)
+ *   string "decodeDefault"    -> an empty payload decodes as the literal
+ *   string "prefix"/"suffix"  -> HasPrefix / HasSuffix, ErrStringPrefix /
+ *                                ErrStringSuffix on decode, ErrEncode on
+ *                                encode (:1070-1158; exact > prefix > suffix)
+ * Encode reports a failing check in the blob's status (bits 24..29 =
+ * the leaf's ErrorCode); the blob's bytes are then not a reference output.
+ * Tuples are always nullable (every STuple* constructor; a "nullable" key is
+ * ignored, schemabuilder_json.go:244-260).
+ * Extensions beyond SchemaJSON (documented, not in the reference's
+ * vocabulary): uint8..uint64 (PutAccess AddUint*) and "sorted" maps.       */
 int  packos_schema_compile(const char* schema_json, int mode, packos_schema** out);
 void packos_schema_free(packos_schema* s);
 int  packos_schema_num_columns(const packos_schema* s);
@@ -171,6 +200,10 @@ int64_t packos_schema_fixed_blob_size(const packos_schema* s);
  * decodes cleanly), else 0.  Decided at compile time, without a GPU; results
  * never depend on it (non-canonical blobs fall back to the exact decoder).  */
 int  packos_schema_decode_fast(const packos_schema* s);
+/* decodeDefault literal of column `col` (a string leaf): copies at most cap
+ * bytes into buf and returns the literal's length (0 = no default, -1 = bad
+ * column).                                                                  */
+int64_t packos_schema_column_default(const packos_schema* s, int col, char* buf, size_t cap);
 /* Host-side dump of the compiled layout program (debug/testing). Returns the
  * number of bytes needed (including NUL); writes at most cap bytes.          */
 size_t packos_schema_describe(const packos_schema* s, char* buf, size_t cap);

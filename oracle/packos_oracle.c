@@ -153,6 +153,33 @@ static const uint8_t* lit_ptr(const or_schema* s, int li, size_t* len) {
     return s->lit + s->lit_off[li];
 }
 
+/* value checks (schema.go:1172-1364 Range, 2188-2250 SDateRange, 1070-1158
+ * CheckFunc Prefix/Suffix, 270-286 DefaultDecodeValue) */
+enum { X_MIN = 1, X_MAX = 2, X_DATE = 4, X_PREFIX = 8, X_SUFFIX = 16, X_DEFAULT = 32 };
+static int64_t xflags(const or_schema* s, int n) { return s->ext ? s->ext[4 * n] : 0; }
+static const uint8_t* xlit(const or_schema* s, int n, int which, size_t* len) {
+    int64_t li = which ? ((s->ext[4 * n + 3] >> 32) & 0xFFFFFFFF) - 1 : (s->ext[4 * n + 3] & 0xFFFFFFFF) - 1;
+    if (li < 0) { *len = 0; return (const uint8_t*)""; }
+    return lit_ptr(s, (int)li, len);
+}
+/* CheckIntRange on the LE value of width w (sign-extended) */
+static int range_bad(const or_schema* s, int n, const uint8_t* p, int w) {
+    int64_t f = xflags(s, n);
+    uint64_t u = 0;
+    for (int b = 0; b < w; b++) u |= (uint64_t)p[b] << (8 * b);
+    int sh = 64 - 8 * w;
+    int64_t v = (int64_t)(u << sh) >> sh;
+    return ((f & X_MIN) && v < s->ext[4 * n + 1]) || ((f & X_MAX) && v > s->ext[4 * n + 2]);
+}
+/* strings.HasPrefix / HasSuffix */
+static int str_bad(const or_schema* s, int n, const uint8_t* p, size_t len) {
+    size_t L;
+    const uint8_t* lit = xlit(s, n, 0, &L);
+    if (len < L) return 1;
+    const uint8_t* at = (xflags(s, n) & X_PREFIX) ? p : p + len - L;
+    return L && memcmp(at, lit, L) != 0;
+}
+
 /* children of a container in emission order; sorted maps order key/value
  * pairs by key bytes (utils.SortKeys = sort.Strings, utils/utils.go:7-14). */
 static int children(const or_schema* s, int n, int* out) {
@@ -294,6 +321,38 @@ int64_t or_encoded_size_one(const or_schema* s, const packos_column* cols, size_
     return sz;
 }
 
+/* EncodeFunc value checks in emission order: the first failing leaf's own
+ * ErrorCode (Range -> ErrOutOfRange, SDateRange -> ErrDateOutOfRange,
+ * CheckFunc -> ErrEncode), 0 if every value passes.  Nil containers and nil
+ * values are not encoded, so not checked (schema.go:1203-1214, 2227-2246,
+ * 1110-1124).                                                                */
+static int enc_check(const or_schema* s, const packos_column* cols, size_t i, int n) {
+    int k = NK(s, n);
+    if (is_container(k)) {
+        int nullable = (k == ORN_MAP) ? 1 : NA(s, n);
+        if (nullable && !col_valid(&cols[s->col_of_node[n]], i)) return 0;
+        int kids[256];
+        int nk = children(s, n, kids);
+        for (int j = 0; j < nk; j++) {
+            int r = enc_check(s, cols, i, kids[j]);
+            if (r) return r;
+        }
+        return 0;
+    }
+    int64_t f = xflags(s, n);
+    if (f & (X_MIN | X_MAX)) {
+        size_t len; int nil; uint8_t tmp[8];
+        const uint8_t* b = leaf_bytes(s, cols, i, n, &len, &nil, tmp);
+        if (nil) return 0;
+        if (range_bad(s, n, b, (int)len)) return (f & X_DATE) ? PACKOS_ERR_DATE_OUT_OF_RANGE : PACKOS_ERR_OUT_OF_RANGE;
+    } else if (f & (X_PREFIX | X_SUFFIX)) {
+        size_t len; int nil; uint8_t tmp[8];
+        const uint8_t* b = leaf_bytes(s, cols, i, n, &len, &nil, tmp);
+        if (str_bad(s, n, b, len)) return PACKOS_ERR_ENCODE;
+    }
+    return 0;
+}
+
 typedef struct enc_tls { or_put p; or_put pool[16]; } enc_tls;
 
 static int64_t encode_one_tls(const or_schema* s, const packos_column* cols, size_t i, int mode,
@@ -357,7 +416,17 @@ static void* enc_worker(void* arg) {
         int o = 0;
         size_t cap = (size_t)(j->offs[i + 1] - j->offs[i]);
         encode_one_tls(j->s, j->cols, i, j->mode, j->out + j->offs[i], cap, &o, &t);
-        if (j->status) j->status[i] = o ? PACKOS_STATUS_OVERFLOW13 : 0u;
+        if (j->status) {
+            uint32_t sv = o ? PACKOS_STATUS_OVERFLOW13 : 0u;
+            for (int tp = 0; j->s->ext && tp < j->s->n_top; tp++) {
+                int inner = enc_check(j->s, j->cols, i, j->s->top_nodes[tp]);
+                if (inner) {
+                    sv |= (uint32_t)PACKOS_ERR_ENCODE | ((uint32_t)(tp + 1) << 8) | ((uint32_t)inner << 24);
+                    break;
+                }
+            }
+            j->status[i] = sv;
+        }
     }
     or_put_free(&t.p);
     for (int d = 0; d < 16; d++) or_put_free(&t.pool[d]);
@@ -504,19 +573,28 @@ static int dec_node(dec_ctx* c, int n, or_seq* q, uint64_t sub_base) {
             if (k == ORN_BOOL) dst[0] = q->buf[ps] != 0;
             else memcpy(dst, q->buf + ps, (size_t)W);
             if (col->valid) col->valid[c->i] = 1;
+            /* Range / SDateRange: CheckIntRange after the Advance */
+            if ((xflags(s, n) & (X_MIN | X_MAX)) && range_bad(s, n, q->buf + ps, W))
+                return (xflags(s, n) & X_DATE) ? PACKOS_ERR_DATE_OUT_OF_RANGE : PACKOS_ERR_OUT_OF_RANGE;
             return 0;
         }
         case ORN_STRING: case ORN_BYTES: {
             int W = NA(s, n);
             int e = prim(q, 6, W, W <= 0, &ps, &w);
             if (e) return e;
+            size_t have = ps < 0 ? 0 : (size_t)w, dl = 0;
+            const uint8_t* dp = (xflags(s, n) & X_DEFAULT) ? xlit(s, n, 1, &dl) : NULL;
+            int dflt = have == 0 && dl > 0;   /* DefaultDecodeVal replaces an empty payload */
             if (W > 0) {
                 memcpy((uint8_t*)col->data + c->i * (size_t)W, q->buf + ps, (size_t)W);
             } else {
                 /* aliasing view like GetStringUnsafe: absolute payload start, 0 for nil */
-                col->start[c->i] = ps < 0 ? 0u : sub_base + (uint64_t)ps;
-                col->length[c->i] = ps < 0 ? 0u : (uint32_t)w;
+                col->start[c->i] = dflt ? PACKOS_VIEW_DEFAULT : ps < 0 ? 0u : sub_base + (uint64_t)ps;
+                col->length[c->i] = dflt ? (uint32_t)dl : (uint32_t)have;
             }
+            if ((xflags(s, n) & (X_PREFIX | X_SUFFIX)) &&
+                str_bad(s, n, dflt ? dp : q->buf + (ps < 0 ? 0 : ps), dflt ? dl : have))
+                return (xflags(s, n) & X_PREFIX) ? PACKOS_ERR_STRING_PREFIX : PACKOS_ERR_STRING_SUFFIX;
             return 0;
         }
         case ORN_MATCH: {
@@ -525,8 +603,11 @@ static int dec_node(dec_ctx* c, int n, or_seq* q, uint64_t sub_base) {
             int e = prim(q, 6, NB(s, n), NB(s, n) <= 0, &ps, &w);
             if (e) return e;
             size_t ll; const uint8_t* lp = lit_ptr(s, NA(s, n), &ll);
-            size_t have = ps < 0 ? 0 : (size_t)w;
-            if (have != ll || (ll && memcmp(q->buf + ps, lp, ll) != 0)) return PACKOS_ERR_STRING_MATCH;
+            size_t have = ps < 0 ? 0 : (size_t)w, dl = 0;
+            const uint8_t* dp = (xflags(s, n) & X_DEFAULT) ? xlit(s, n, 1, &dl) : NULL;
+            const uint8_t* vp = q->buf + (ps < 0 ? 0 : ps);
+            if (have == 0 && dl > 0) { vp = dp; have = dl; }
+            if (have != ll || (ll && memcmp(vp, lp, ll) != 0)) return PACKOS_ERR_STRING_MATCH;
             return 0;
         }
         case ORN_TUPLE: case ORN_MAP: {

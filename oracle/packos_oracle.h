@@ -75,6 +75,12 @@ typedef struct or_schema {
     int32_t        col_of_node[512];
     int32_t        next_sibling[512];
     int32_t        top_nodes[256];
+    /* optional value checks, 4 int64 per node (NULL = none):
+     *   [0] flags: 1 min, 2 max, 4 date (ErrDateOutOfRange), 8 prefix,
+     *       16 suffix, 32 decodeDefault       (same bits as CHK_* in the product)
+     *   [1] min  [2] max
+     *   [3] (prefix/suffix literal index + 1) | (default literal index + 1) << 32 */
+    const int64_t* ext;
 } or_schema;
 
 int or_schema_prepare(or_schema* s);   /* 0 ok */

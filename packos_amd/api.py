@@ -99,6 +99,15 @@ class CompiledSchema:
         return int(lib().packos_schema_blob_size_host(
             self._h, None if w is None else w.ctypes.data, None if v is None else v.ctypes.data))
 
+    def column_default(self, c: int) -> bytes:
+        """decodeDefault literal of column c (b"" when it has none)."""
+        n = int(lib().packos_schema_column_default(self._h, c, None, 0))
+        if n <= 0:
+            return b""
+        buf = C.create_string_buffer(n)
+        lib().packos_schema_column_default(self._h, c, buf, n)
+        return buf.raw[:n]
+
     def describe(self) -> str:
         n = lib().packos_schema_describe(self._h, None, 0)
         buf = C.create_string_buffer(n)
@@ -325,6 +334,17 @@ class DecodedColumns:
             self.start.append(torch.zeros(max(n, 1), dtype=torch.int64, device=device) if sp.var else None)
             self.length.append(torch.zeros(max(n, 1), dtype=torch.int32, device=device) if sp.var else None)
 
+    def var_values(self, c: int, arena) -> List[bytes]:
+        """Bytes of var column c per blob (host copy): the arena slice each view
+        aliases, or the schema's decodeDefault literal for PACKOS_VIEW_DEFAULT
+        views (what DecodeBuffer returns, schema/schema.go:279-286)."""
+        a = arena.cpu().numpy() if hasattr(arena, "cpu") else np.asarray(arena)
+        st = self.start[c][: self.n].cpu().numpy().view(np.uint64)
+        ln = self.length[c][: self.n].cpu().numpy().view(np.uint32)
+        dflt = self.schema.column_default(c)
+        return [dflt if int(s0) == VIEW_DEFAULT else bytes(a[int(s0): int(s0) + int(l0)])
+                for s0, l0 in zip(st, ln)]
+
     def ctypes_array(self):
         arr = (PackosColumn * max(1, len(self.schema.specs)))()
         for c in range(len(self.schema.specs)):
@@ -373,6 +393,9 @@ def get_field_batch(arena, offsets, n: int, path, want_tag: int, want_width: int
           "packos_get_field_batch")
     return s0[:n], ln[:n], tg[:n], st[:n]
 
+
+# decode view of an empty string payload replaced by its decodeDefault (include/packos.h)
+VIEW_DEFAULT = 0x8000000000000000
 
 # getter families of packos_get_batch (include/packos.h)
 GET_FIXED, GET_NULLABLE, GET_SPAN, GET_INT, GET_FLOAT = range(5)

@@ -72,6 +72,9 @@ def scalar_bytes(node: Schema, v) -> bytes:
     if k == "bool":
         return b"\x01" if v else b"\x00"
     if k in ("int", "uint"):
+        if hasattr(v, "timestamp"):   # SDateRange encodes time.Time as Unix() seconds
+            import math
+            v = math.floor(v.timestamp())
         return (int(v) & ((1 << (8 * w)) - 1)).to_bytes(w, "little")
     if k == "float":
         if isinstance(v, (bytes, bytearray)):

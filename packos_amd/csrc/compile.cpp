@@ -7,6 +7,8 @@
 // header-block sizes (access/put.go:619-627, packable/pack.go:36) and, for
 // fixed-size schemas, every header word of the blob.
 #include <algorithm>
+#include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <sstream>
 
@@ -70,6 +72,75 @@ struct Builder {
         return (v && v->kind == JVal::NUM) ? (int)v->num : 0;
     }
 
+    // SchemaJSON Min/Max are *int64 (schemabuilder_json.go:18-19): an exact
+    // integer literal, or absent / null
+    static bool int64_field(const JVal& j, const char* k, int64_t* out) {
+        const JVal* v = j.get(k);
+        if (!v || v->kind == JVal::NUL) return false;
+        if (v->kind != JVal::NUM || v->str.find_first_of(".eE") != std::string::npos)
+            fail(PACKOS_E_SCHEMA, std::string("'") + k + "' must be an integer");
+        errno = 0;
+        char* end = nullptr;
+        long long x = strtoll(v->str.c_str(), &end, 10);
+        if (errno || !end || *end) fail(PACKOS_E_SCHEMA, std::string("'") + k + "' is not an int64");
+        *out = (int64_t)x;
+        return true;
+    }
+
+    // time.Parse(time.RFC3339, s).Unix(); the builder drops the parse error
+    // (schemabuilder_json.go:169-170), so a bad string is the zero Time,
+    // whose Unix() is -62135596800.
+    static int64_t rfc3339_unix(const std::string& t) {
+        const int64_t zero = -62135596800LL;
+        auto dig = [&](size_t at, int n, int* v) {
+            if (at + n > t.size()) return false;
+            int x = 0;
+            for (int k = 0; k < n; k++) {
+                char c = t[at + k];
+                if (c < '0' || c > '9') return false;
+                x = 10 * x + (c - '0');
+            }
+            *v = x;
+            return true;
+        };
+        int Y, M, D, h, m, sec;
+        if (!dig(0, 4, &Y) || t.size() < 20 || t[4] != '-' || !dig(5, 2, &M) || t[7] != '-' || !dig(8, 2, &D) ||
+            t[10] != 'T' || !dig(11, 2, &h) || t[13] != ':' || !dig(14, 2, &m) || t[16] != ':' || !dig(17, 2, &sec))
+            return zero;
+        size_t p = 19;
+        if (p < t.size() && t[p] == '.') {   // fractional seconds: dropped by Unix()
+            size_t q = p + 1;
+            while (q < t.size() && t[q] >= '0' && t[q] <= '9') q++;
+            if (q == p + 1) return zero;
+            p = q;
+        }
+        int64_t tz = 0;
+        if (p < t.size() && t[p] == 'Z') {
+            p++;
+        } else if (p < t.size() && (t[p] == '+' || t[p] == '-')) {
+            int th, tm;
+            if (!dig(p + 1, 2, &th) || p + 3 >= t.size() || t[p + 3] != ':' || !dig(p + 4, 2, &tm) || th > 23 || tm > 59)
+                return zero;
+            tz = (t[p] == '-' ? -1 : 1) * (int64_t)(th * 3600 + tm * 60);
+            p += 6;
+        } else {
+            return zero;
+        }
+        if (p != t.size()) return zero;
+        static const int mdays[12] = {31, 29, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+        const bool leap = (Y % 4 == 0 && Y % 100 != 0) || Y % 400 == 0;
+        if (M < 1 || M > 12 || D < 1 || D > mdays[M - 1] || (M == 2 && D == 29 && !leap) || h > 23 || m > 59 || sec > 59)
+            return zero;
+        // days from civil (proleptic Gregorian)
+        const int y = Y - (M <= 2);
+        const int era = (y >= 0 ? y : y - 399) / 400;
+        const int yoe = y - era * 400;
+        const int doy = (153 * (M + (M > 2 ? -3 : 9)) + 2) / 5 + D - 1;
+        const int doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+        const int64_t days = (int64_t)era * 146097 + doe - 719468;
+        return days * 86400 + h * 3600 + m * 60 + sec - tz;
+    }
+
     // BuildSchema (schemabuilder_json.go:124-300), compiled subset
     int node(const JVal& j, int parent, int depth, int top, const std::string& name) {
         if (j.kind != JVal::OBJ) fail(PACKOS_E_SCHEMA, "schema node must be an object");
@@ -94,29 +165,66 @@ struct Builder {
             Node& n = s->nodes[id];
             n.kind = K_BOOL; n.width = 1; n.nullable = nullable;
         } else if (t.rfind("int", 0) == 0 && width_of(t.c_str() + 3)) {
-            unsupported_keys({"min", "max"});
             Node& n = s->nodes[id];
             n.kind = K_INT; n.width = width_of(t.c_str() + 3); n.nullable = nullable;
+            // int16/32/64 with Min or Max -> s.Range(min, max), whose precheck
+            // is never nullable (schema.go:1175-1364); int8 ignores them
+            // (schemabuilder_json.go:133-137)
+            int64_t lo = 0, hi = 0;
+            const bool has_lo = int64_field(j, "min", &lo), has_hi = int64_field(j, "max", &hi);
+            if (n.width > 1 && (has_lo || has_hi)) {
+                n.nullable = false;
+                n.check = (has_lo ? CHK_MIN : 0u) | (has_hi ? CHK_MAX : 0u);
+                n.rmin = lo;
+                n.rmax = hi;
+            }
+        } else if (t == "date") {
+            // SDateRange(nullable, from, to): int64 payload, bounds only when
+            // both dates are given (schemabuilder_json.go:166-173, schema.go:2188-2250)
+            Node& n = s->nodes[id];
+            n.kind = K_INT; n.width = 8; n.nullable = nullable;
+            n.check = CHK_DATE;
+            const std::string from = str_field(j, "dateFrom"), to = str_field(j, "dateTo");
+            if (!from.empty() && !to.empty()) {
+                n.check |= CHK_RANGE;
+                n.rmin = rfc3339_unix(from);
+                n.rmax = rfc3339_unix(to);
+            }
         } else if (t.rfind("uint", 0) == 0 && width_of(t.c_str() + 4)) {
+            unsupported_keys({"min", "max"});
             Node& n = s->nodes[id];
             n.kind = K_UINT; n.width = width_of(t.c_str() + 4); n.nullable = nullable;
         } else if (t == "float32" || t == "float64") {
             Node& n = s->nodes[id];
             n.kind = K_FLOAT; n.width = t == "float32" ? 4 : 8; n.nullable = nullable;
         } else if (t == "string") {
-            unsupported_keys({"prefix", "suffix", "pattern", "decodeDefault"});
-            // SString / Optional() (Width -1) / WithWidth(n) (schemabuilder_json.go:184-208)
+            // SString / Optional() (Width -1) / WithWidth(n), then
+            // DefaultDecodeValue, then the first of exact / prefix / suffix /
+            // pattern (schemabuilder_json.go:184-208)
             int w = 0;
             if (nullable) w = -1;
             else if (int_field(j, "width") > 0) w = int_field(j, "width");
             Node& n = s->nodes[id];
             n.width = w;
             n.nullable = w <= 0;
-            if (j.get("exact") && !str_field(j, "exact").empty()) {
+            n.dflt = str_field(j, "decodeDefault");
+            if (!n.dflt.empty()) n.check |= CHK_DEFAULT;
+            const std::string exact = str_field(j, "exact"), prefix = str_field(j, "prefix"),
+                              suffix = str_field(j, "suffix"), pattern = str_field(j, "pattern");
+            if (!exact.empty()) {
                 n.kind = K_MATCH;
-                n.literal = str_field(j, "exact");
+                n.literal = exact;
             } else {
                 n.kind = K_STRING;
+                if (!prefix.empty()) {
+                    n.check |= CHK_PREFIX;
+                    n.check_lit = prefix;
+                } else if (!suffix.empty()) {
+                    n.check |= CHK_SUFFIX;
+                    n.check_lit = suffix;
+                } else if (!pattern.empty()) {
+                    fail(PACKOS_E_UNSUPPORTED, "'pattern' (regexp) strings are outside the compiled subset");
+                }
             }
         } else if (t == "bytes") {
             int w = int_field(j, "width");
@@ -129,7 +237,10 @@ struct Builder {
             {
                 Node& n = s->nodes[id];
                 n.kind = K_TUPLE;
-                n.nullable = bool_field(j, "nullable", true);  // STuple* are Nullable: true
+                // every STuple* constructor sets Nullable: true and BuildSchema
+                // never reads the key for tuples (schemabuilder_json.go:244-260,
+                // schema.go:1551-1552)
+                n.nullable = true;
                 n.variable = bool_field(j, "variableLength");
             }
             if (sch && sch->kind == JVal::ARR) {
@@ -263,6 +374,7 @@ struct Builder {
                 it.is_bool = n.kind == K_BOOL;
                 s->items.push_back(it);
                 if (n.nullable) s->has_nullable = true;
+                add_check(n, cont_id);
                 return;
             case K_STRING: case K_BYTES:
                 if (n.width > 0) {
@@ -273,6 +385,7 @@ struct Builder {
                     s->has_var = true;
                 }
                 s->items.push_back(it);
+                add_check(n, cont_id);
                 return;
             case K_MATCH:
                 it.type = IT_CONST;
@@ -298,8 +411,34 @@ struct Builder {
         fail(PACKOS_E_SCHEMA, "bad node");
     }
 
+    // EncodeFunc value checks, in emission order (EncodeValue stops at the
+    // first failing field): Range -> ErrOutOfRange (schema.go:1205-1212),
+    // SDateRange -> ErrDateOutOfRange (:2231-2246), CheckFunc Prefix/Suffix ->
+    // ErrEncode (:1110-1124)
+    void add_check(const Node& n, int cont_id) {
+        const uint32_t f = n.check & (CHK_RANGE | CHK_STR);
+        if (!f) return;
+        EncCheck c{};
+        c.col = n.col;
+        c.cont = cont_id;
+        c.top = n.top;
+        c.flags = n.check;
+        c.width = n.width > 0 ? (uint32_t)n.width : 0u;
+        c.rmin = n.rmin;
+        c.rmax = n.rmax;
+        if (f & CHK_STR) {
+            c.lit = (uint32_t)s->lits.size();
+            c.lit_len = (uint32_t)n.check_lit.size();
+            s->lits.insert(s->lits.end(), n.check_lit.begin(), n.check_lit.end());
+            c.inner = PACKOS_ERR_ENCODE;
+        } else {
+            c.inner = (n.check & CHK_DATE) ? PACKOS_ERR_DATE_OUT_OF_RANGE : PACKOS_ERR_OUT_OF_RANGE;
+        }
+        s->echk.push_back(c);
+    }
+
     void build_encode() {
-        s->items.clear(); s->hdrs.clear(); s->conts.clear(); s->lits.clear();
+        s->items.clear(); s->hdrs.clear(); s->conts.clear(); s->lits.clear(); s->echk.clear();
         EncCont root{};
         root.parent = -1;
         root.valid_col = -1;
@@ -437,6 +576,19 @@ struct Builder {
             df.flags = bm[df.blob_off].is_bool ? 1u : 0u;
             df.magic = fc.width > 1 ? (uint32_t)(((1ull << 32) + fc.width - 1) / fc.width) : 0u;
             s->dfix.push_back(df);
+        }
+        s->dvchk.clear();
+        for (const EncCheck& c : s->echk) {
+            DecChk v{};
+            for (const DecFix& df : s->dfix)
+                if (df.col == c.col) v.blob_off = df.blob_off;
+            v.width = (uint32_t)s->nodes[s->col_node[c.col]].width;
+            v.flags = c.flags;
+            v.lit = c.lit;
+            v.lit_len = c.lit_len;
+            v.rmin = c.rmin;
+            v.rmax = c.rmax;
+            s->dvchk.push_back(v);
         }
         if (s->fix_lds > 60 * 1024) return;
         // segments for each dword r of a 4-blob period
@@ -593,6 +745,18 @@ struct Builder {
                 d.lit = (uint32_t)s->lits.size();
                 d.lit_len = (uint32_t)n.literal.size();
                 s->lits.insert(s->lits.end(), n.literal.begin(), n.literal.end());
+            } else if (n.check & CHK_STR) {
+                d.lit = (uint32_t)s->lits.size();
+                d.lit_len = (uint32_t)n.check_lit.size();
+                s->lits.insert(s->lits.end(), n.check_lit.begin(), n.check_lit.end());
+            }
+            d.check = n.check;
+            d.rmin = n.rmin;
+            d.rmax = n.rmax;
+            if (n.check & CHK_DEFAULT) {
+                d.dlit = (uint32_t)s->lits.size();
+                d.dlit_len = (uint32_t)n.dflt.size();
+                s->lits.insert(s->lits.end(), n.dflt.begin(), n.dflt.end());
             }
         }
     }
@@ -635,6 +799,9 @@ struct Builder {
             o << "item " << i << " " << tn[it.type] << " cont=" << it.cont << " col=" << it.col
               << " size=" << it.size << (it.nullable ? " nullable" : "") << (it.is_bool ? " bool" : "") << "\n";
         }
+        for (const EncCheck& c : s->echk)
+            o << "check col=" << c.col << " cont=" << c.cont << " top=" << c.top << " flags=" << c.flags
+              << " min=" << c.rmin << " max=" << c.rmax << " lit_len=" << c.lit_len << " inner=" << c.inner << "\n";
         for (const EncHdr& h : s->hdrs)
             o << "hdr cont=" << h.cont << " j=" << h.j << " tag=" << (int)h.tag
               << (h.relative ? " rel target=" : " const=") << (h.relative ? h.target : h.value) << "\n";
@@ -749,6 +916,14 @@ int packos_schema_decode_fast(const packos_schema* s) { return s && s->dec_fast 
 int64_t packos_schema_fixed_blob_size(const packos_schema* s) {
     if (!s || s->has_var) return -1;
     return s->all_present_size;
+}
+
+int64_t packos_schema_column_default(const packos_schema* s, int col, char* buf, size_t cap) {
+    if (!s || col < 0 || col >= (int)s->col_node.size()) return -1;
+    const Node& n = s->nodes[s->col_node[col]];
+    if (!(n.check & CHK_DEFAULT)) return 0;
+    if (buf && cap) memcpy(buf, n.dflt.data(), std::min(cap, n.dflt.size()));
+    return (int64_t)n.dflt.size();
 }
 
 size_t packos_schema_describe(const packos_schema* s, char* buf, size_t cap) {

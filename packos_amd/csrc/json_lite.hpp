@@ -14,7 +14,7 @@ struct JVal {
     enum Kind { NUL, BOOL, NUM, STR, ARR, OBJ } kind = NUL;
     bool b = false;
     double num = 0;
-    std::string str;
+    std::string str;        // STR: the string; NUM: the literal's text (exact int64 parsing)
     std::vector<JVal> arr;
     std::vector<std::pair<std::string, JVal>> obj;
 
@@ -95,7 +95,8 @@ private:
                                       s_[i_] == 'E' || s_[i_] == '+' || s_[i_] == '-'))
                 i_++;
             v.kind = JVal::NUM;
-            v.num = std::stod(s_.substr(st, i_ - st));
+            v.str = s_.substr(st, i_ - st);
+            v.num = std::stod(v.str);
             return v;
         }
         fail("unexpected character");

@@ -516,6 +516,54 @@ __global__ __launch_bounds__(kBlock) void k_encode_var(EncProgram P, EncCols col
         var_blob_wave(P, cols, i, offs ? offs[i] : i * stride, out, cap, status, slot, pos, lane);
 }
 
+// EncodeFunc value checks (Range / SDateRange / CheckFunc Prefix-Suffix),
+// one thread per blob, after the encode kernel on the same stream.  The first
+// failing check in emission order wins (EncodeValue stops there); values
+// inside a nil container or nil themselves are not encoded, so not checked.
+// Passing blobs are not touched; a failing blob's status becomes ErrEncode at
+// its top-level field with the leaf's code in bits 24..29.
+__global__ __launch_bounds__(kBlock) void k_encode_checks(const EncCheck* __restrict__ chk, int nchk, EncProgram P,
+                                                          EncCols cols, uint64_t n, uint32_t* __restrict__ status,
+                                                          int need_pm) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t pm = need_pm ? present_mask(P, cols, i) : ~0ull;
+    for (int k = 0; k < nchk; k++) {
+        const EncCheck c = chk[k];
+        if (!((pm >> c.cont) & 1ull)) continue;
+        bool bad;
+        if (c.flags & CHK_RANGE) {
+            const uint8_t* v = cols.valid[c.col];
+            if (v && !v[i]) continue;
+            const uint8_t* p = cols.data[c.col] + i * (uint64_t)c.width;
+            uint64_t u = 0;
+            for (uint32_t b = 0; b < c.width; b++) u |= (uint64_t)p[b] << (8 * b);
+            const int sh = 64 - 8 * (int)c.width;
+            const int64_t x = (int64_t)(u << sh) >> sh;
+            bad = ((c.flags & CHK_MIN) && x < c.rmin) || ((c.flags & CHK_MAX) && x > c.rmax);
+        } else {
+            const uint8_t* p;
+            uint64_t len;
+            if (c.width) {
+                p = cols.data[c.col] + i * (uint64_t)c.width;
+                len = c.width;
+            } else {
+                const uint64_t a = col_off(cols, c.col, i);
+                p = cols.data[c.col] + a;
+                len = col_off(cols, c.col, i + 1) - a;
+            }
+            bad = len < c.lit_len;
+            const uint64_t at = (c.flags & CHK_PREFIX) ? 0ull : len - c.lit_len;
+            for (uint32_t b = 0; !bad && b < c.lit_len; b++) bad = p[at + b] != P.lits[c.lit + b];
+        }
+        if (bad) {
+            status[i] = (status[i] & (PACKOS_STATUS_PANIC | PACKOS_STATUS_OVERFLOW13)) | (uint32_t)PACKOS_ERR_ENCODE |
+                        ((uint32_t)(c.top + 1) << 8) | (c.inner << 24);
+            return;
+        }
+    }
+}
+
 typedef __attribute__((address_space(1))) const uint32_t g_u32;
 typedef __attribute__((address_space(1))) const uint64_t g_u64;
 typedef __attribute__((address_space(1))) const uint8_t g_u8;
@@ -682,6 +730,9 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
             if (a) { err = a == 2 ? kPanic : 2; break; }
         }
         const uint64_t pay = q.start + (ps < 0 ? 0 : ps);
+        const uint32_t have = ps < 0 ? 0u : (uint32_t)w;
+        // DefaultDecodeValue: an empty payload reads as the literal (schema.go:283-285)
+        const bool dflt = have == 0 && (nd.check & CHK_DEFAULT) && nd.dlit_len > 0;
         switch (nd.kind) {
             case K_INT: case K_UINT: case K_FLOAT: case K_BOOL: {
                 if (ps < 0) {
@@ -693,6 +744,14 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
                 if (nd.kind == K_BOOL) dstp[0] = arena(pay) != 0;
                 else copy_out(dstp, arena, pay, (uint32_t)nd.width);
                 if (cols.valid[nd.col]) cols.valid[nd.col][i] = 1;
+                if (nd.check & CHK_RANGE) {   // CheckIntRange after Advance (schema.go:1187-1201, 2213-2224)
+                    uint64_t u = 0;
+                    for (int b = 0; b < nd.width; b++) u |= (uint64_t)arena(pay + b) << (8 * b);
+                    const int sh = 64 - 8 * nd.width;
+                    const int64_t v = (int64_t)(u << sh) >> sh;
+                    if (((nd.check & CHK_MIN) && v < nd.rmin) || ((nd.check & CHK_MAX) && v > nd.rmax))
+                        err = (nd.check & CHK_DATE) ? PACKOS_ERR_DATE_OUT_OF_RANGE : PACKOS_ERR_OUT_OF_RANGE;
+                }
                 break;
             }
             case K_STRING: case K_BYTES:
@@ -700,14 +759,25 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
                     uint8_t* dstp = cols.data[nd.col] + i * (uint64_t)nd.width;
                     copy_out(dstp, arena, pay, (uint32_t)nd.width);
                 } else {
-                    cols.start[nd.col][i] = ps < 0 ? 0ull : q.start + (uint64_t)ps;
-                    cols.length[nd.col][i] = ps < 0 ? 0u : (uint32_t)w;
+                    cols.start[nd.col][i] = dflt ? PACKOS_VIEW_DEFAULT : ps < 0 ? 0ull : q.start + (uint64_t)ps;
+                    cols.length[nd.col][i] = dflt ? nd.dlit_len : have;
+                }
+                if (nd.check & CHK_STR) {   // CheckFunc DecodeFunc: HasPrefix / HasSuffix (schema.go:1093-1108)
+                    const uint32_t len = dflt ? nd.dlit_len : have, L = nd.lit_len;
+                    bool ok = len >= L;
+                    const uint32_t at = (nd.check & CHK_PREFIX) ? 0u : len - L;
+                    for (uint32_t j = 0; ok && j < L; j++) {
+                        const uint32_t c = dflt ? P.lits[nd.dlit + at + j] : arena(pay + at + j);
+                        ok = c == P.lits[nd.lit + j];
+                    }
+                    if (!ok) err = (nd.check & CHK_PREFIX) ? PACKOS_ERR_STRING_PREFIX : PACKOS_ERR_STRING_SUFFIX;
                 }
                 break;
             case K_MATCH: {
-                const uint32_t have = ps < 0 ? 0u : (uint32_t)w;
-                bool eq = have == nd.lit_len;
-                for (uint32_t j = 0; eq && j < have; j++) eq = arena(pay + j) == P.lits[nd.lit + j];
+                const uint32_t len = dflt ? nd.dlit_len : have;
+                bool eq = len == nd.lit_len;
+                for (uint32_t j = 0; eq && j < len; j++)
+                    eq = (dflt ? P.lits[nd.dlit + j] : arena(pay + j)) == P.lits[nd.lit + j];
                 if (!eq) err = PACKOS_ERR_STRING_MATCH;
                 break;
             }
@@ -882,6 +952,26 @@ __global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecPro
             const uint32_t v = (B & 3) == 0 ? lds[a >> 2] : lds_bytes4(lds, a);
             if ((v & c[1]) != c[2]) fail[j] = 1;
         }
+    }
+    // 2b. value checks of fixed leaves (Range, Prefix/Suffix of fixed strings):
+    //    a failing row takes the exact per-blob path, which reports it
+    for (uint32_t e = tid; e < rows * (uint32_t)F.n_vchk; e += kBlock) {
+        const uint32_t j = e / (uint32_t)F.n_vchk;
+        const DecChk c = F.vchk[e - j * (uint32_t)F.n_vchk];
+        const uint32_t a = j * B + c.blob_off;
+        bool bad;
+        if (c.flags & CHK_RANGE) {
+            uint64_t u = 0;
+            for (uint32_t b = 0; b < c.width; b++) u |= (uint64_t)lds_u8(lds, a + b) << (8 * b);
+            const int sh = 64 - 8 * (int)c.width;
+            const int64_t v = (int64_t)(u << sh) >> sh;
+            bad = ((c.flags & CHK_MIN) && v < c.rmin) || ((c.flags & CHK_MAX) && v > c.rmax);
+        } else {
+            bad = c.lit_len > c.width;
+            const uint32_t at = (c.flags & CHK_PREFIX) ? 0u : c.width - c.lit_len;
+            for (uint32_t b = 0; !bad && b < c.lit_len; b++) bad = lds_u8(lds, a + at + b) != P.lits[c.lit + b];
+        }
+        if (bad) fail[j] = 1;
     }
     // 3. columns: uniform walk over the columns; threads stride the column's
     //    output dwords (consecutive lanes -> consecutive dwords: 256-B stores)
@@ -1088,7 +1178,12 @@ bool packos::canonical_decodes(const packos_schema* s) {
         dc.start[c] = &start[c];
         dc.length[c] = &length[c];
     }
-    DecProgram P{s->dnodes.data(), s->dkids.data(), s->lits.data(), 0, (int32_t)s->dnodes.size(),
+    // structure only: value checks (ranges, prefixes) of the zero payloads are
+    // not the question here; k_decode_fixed re-checks every row's values and
+    // sends failing rows to decode_blob
+    std::vector<DecNode> nodes = s->dnodes;
+    for (DecNode& d : nodes) d.check &= ~(uint32_t)(CHK_RANGE | CHK_STR);
+    DecProgram P{nodes.data(), s->dkids.data(), s->lits.data(), 0, (int32_t)nodes.size(),
                  (int32_t)s->dkids.size(), (int32_t)s->lits.size()};
     return decode_blob(P, dc, GReader{s->canon.data()}, 0, s->canon.size(), 0) == 0;
 }
@@ -1152,6 +1247,8 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     size_t o_dkids = put_bytes(blob, s->dkids);
     size_t o_dfix = put_bytes(blob, s->dfix);
     size_t o_dchk = put_bytes(blob, s->dchk);
+    size_t o_dvchk = put_bytes(blob, s->dvchk);
+    size_t o_echk = put_bytes(blob, s->echk);
     DeviceTables t;
     t.device = device;
     HIP_TRY(hipMalloc(&t.block, blob.size()));
@@ -1192,6 +1289,9 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     t.dec.n_lits = (int32_t)s->lits.size();
     t.dfix.cols = (const DecFix*)(b + o_dfix);
     t.dfix.chk = (const uint32_t*)(b + o_dchk);
+    t.dfix.vchk = (const DecChk*)(b + o_dvchk);
+    t.dfix.n_vchk = (int32_t)s->dvchk.size();
+    t.echk = (const EncCheck*)(b + o_echk);
     t.dfix.n_chk = (int32_t)(s->dchk.size() / 3);
     t.dfix.B = (int)s->all_present_size;
     t.dfix.T = s->fix_T;
@@ -1302,6 +1402,10 @@ int packos_encoded_size_batch(const packos_schema* cs, const packos_column* cols
     return size_pass(s, t, ec, n, out_offsets, ws, ws_bytes, st);
 }
 
+static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& ec, bool any_nil, size_t n,
+                             uint8_t* out, uint64_t cap, uint64_t* out_offsets, uint32_t* status, void* ws,
+                             size_t ws_bytes, uint32_t flags, hipStream_t st);
+
 int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size_t n, uint8_t* out, uint64_t cap,
                         uint64_t* out_offsets, uint32_t* status, void* ws, size_t ws_bytes, uint32_t flags,
                         void* stream) {
@@ -1319,6 +1423,22 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
     bool any_nil;
     if ((r = fill_enc_cols(s, cols, ec, &any_nil))) return r;
     hipStream_t st = (hipStream_t)stream;
+    if ((r = encode_batch_impl(s, t, ec, any_nil, n, out, cap, out_offsets, status, ws, ws_bytes, flags, st)))
+        return r;
+    if (status && !s->echk.empty()) {
+        bool pm = false;
+        for (const EncCont& c : s->conts) pm = pm || (c.valid_col >= 0 && ec.valid[c.valid_col]);
+        hipLaunchKernelGGL(k_encode_checks, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, t->echk,
+                           (int)s->echk.size(), t->enc, ec, (uint64_t)n, status, pm ? 1 : 0);
+        HIP_TRY(hipGetLastError());
+    }
+    return PACKOS_OK;
+}
+
+static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& ec, bool any_nil, size_t n,
+                             uint8_t* out, uint64_t cap, uint64_t* out_offsets, uint32_t* status, void* ws,
+                             size_t ws_bytes, uint32_t flags, hipStream_t st) {
+    int r;
     const bool fixed_size = !s->has_var && !any_nil;
     if (fixed_size) {
         const uint64_t B = (uint64_t)s->all_present_size;
@@ -1410,6 +1530,8 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
         const uint64_t ntiles = (n + kVT - 1) / kVT;
 #ifdef PACKOS_PHASE_PROF
         static unsigned long long* prof[64] = {};
+        int dev = 0;
+        HIP_TRY(hipGetDevice(&dev));
         if (!prof[dev]) HIP_TRY(hipMalloc(&prof[dev], 8 * sizeof(unsigned long long)));
         HIP_TRY(hipMemsetAsync(prof[dev], 0, 8 * sizeof(unsigned long long), st));
         V.prof = prof[dev];

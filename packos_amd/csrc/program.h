@@ -14,6 +14,31 @@ enum NodeKind : int32_t {
     K_MATCH = 7, K_TUPLE = 8, K_MAP = 9, K_ROOT = 10
 };
 
+// Value checks of a leaf (schema-level constraints on top of the wire format).
+enum : uint32_t {
+    CHK_MIN = 1u,        // int value >= rmin        (SInt*.Range / SDateRange)
+    CHK_MAX = 2u,        // int value <= rmax
+    CHK_DATE = 4u,       // range error is ErrDateOutOfRange, not ErrOutOfRange
+    CHK_PREFIX = 8u,     // strings.HasPrefix(value, lit)   -> ErrStringPrefix
+    CHK_SUFFIX = 16u,    // strings.HasSuffix(value, lit)   -> ErrStringSuffix
+    CHK_DEFAULT = 32u,   // empty payload decodes as the default literal
+    CHK_RANGE = CHK_MIN | CHK_MAX,
+    CHK_STR = CHK_PREFIX | CHK_SUFFIX,
+};
+
+// One encode-time value check (EncodeFunc of Range / SDateRange / CheckFunc),
+// evaluated per blob by k_encode_checks after the encode kernel.
+struct EncCheck {
+    int32_t col;         // leaf column
+    int32_t cont;        // container whose presence gates the value
+    int32_t top;         // top-level field index (status position)
+    uint32_t flags;      // CHK_*
+    uint32_t width;      // int width (range) / fixed string width (0 = var)
+    uint32_t lit, lit_len;
+    uint32_t inner;      // schema ErrorCode of the leaf's own error
+    int64_t rmin, rmax;
+};
+
 // ---------------------------------------------------------------- encode ----
 // Items are the byte runs of one blob in wire order.  Positions are the
 // exclusive prefix sum of item sizes; header words are differences of
@@ -146,7 +171,11 @@ struct DecNode {
     uint8_t variable;  // TupleSchema.VariableLength
     uint8_t tag;
     uint8_t pad;
-    uint32_t lit, lit_len;
+    uint32_t lit, lit_len;    // K_MATCH literal, or the Prefix / Suffix literal
+    uint32_t check;           // CHK_* value checks
+    uint32_t dlit, dlit_len;  // DefaultDecodeValue literal (CHK_DEFAULT)
+    uint32_t pad2;
+    int64_t rmin, rmax;       // CHK_MIN / CHK_MAX bounds
 };
 
 struct DecProgram {
@@ -170,14 +199,23 @@ struct DecFix {
     uint32_t pad[3];
 };
 
+// Value check of a fixed leaf in the fixed-layout decode fast path: a row
+// that fails it is re-decoded by the exact per-blob decoder (which reports it).
+struct DecChk {
+    uint32_t blob_off, width, flags, lit, lit_len, pad;
+    int64_t rmin, rmax;
+};
+
 struct DecFixProgram {
     const DecFix* cols;
+    const DecChk* vchk;    // n_vchk value checks
     const uint32_t* chk;   // n_chk triples {blob dword q, constant-byte mask, constant value}, mask != 0
     int32_t B, T, n_cols, pad;
     uint32_t q_magic;      // B % 4 == 0: ceil(2^32 / (B/4)) (0 when B/4 == 1)
     uint32_t b_magic;      // B % 4 != 0: ceil(2^32 / B)
     int32_t n_all_cols;    // every schema column (validity marking)
     int32_t n_chk;
+    int32_t n_vchk;
 };
 
 // column pointer tables passed by value as kernel arguments

@@ -17,6 +17,12 @@ struct Node {
     bool variable = false; // TupleSchema.VariableLength
     bool sorted = false;   // map pairs sorted by key (PackMapSorted)
     std::string literal;   // K_MATCH
+    // value checks (schema.go:1172-1364 Range, :2188-2250 SDateRange,
+    // :1070-1158 CheckFunc Prefix/Suffix, :284-286 DefaultDecodeValue)
+    uint32_t check = 0;    // CHK_* bits (program.h)
+    int64_t rmin = 0, rmax = 0;
+    std::string check_lit; // Prefix / Suffix literal
+    std::string dflt;      // SchemaString.DefaultDecodeVal
     std::vector<int> kids; // emission order
     std::string name;      // dotted field path
     int col = -1;
@@ -45,6 +51,7 @@ struct DeviceTables {
     FixProgram fix{};
     DecProgram dec{};
     DecFixProgram dfix{};
+    const EncCheck* echk = nullptr;
 };
 
 }  // namespace packos
@@ -63,6 +70,7 @@ struct packos_schema {
     std::vector<packos::EncHdr> hdrs;
     std::vector<packos::EncCont> conts;
     std::vector<uint8_t> lits;
+    std::vector<packos::EncCheck> echk;   // encode-time value checks (emission order)
     bool has_var = false;        // any var-width leaf
     bool has_nullable = false;   // any nullable leaf / container column
     int64_t all_present_size = -1;  // blob size when every nullable is present (no var leaves)
@@ -86,6 +94,7 @@ struct packos_schema {
     // fixed-layout decode fast path (B % 4 == 0, B <= 1024); dec_fast is set
     // when the canonical blob decodes cleanly (checked on first upload)
     std::vector<packos::DecFix> dfix;
+    std::vector<packos::DecChk> dvchk;    // value checks of fixed leaves
     std::vector<uint32_t> dchk;
     std::vector<uint8_t> canon;       // all-present blob, zero payload bytes
     int dec_fast = 0;                 // 1: canonical blob decodes (set at compile)

@@ -11,6 +11,9 @@ against the reference reads the same here:
 * ``SMap(*schemas)`` — :858 (key, value, key, value ...)
 * ``STuple``, ``STupleVal``, ``STupleNamed``, ``STupleNamedVal`` — :1551-1699
 * ``SChain`` / ``SchemaNamedChain`` — :1054-1059, :943-946
+* value checks: ``SInt16/32/64.Range(min, max)`` / ``.RangeValues`` (:1172-1364),
+  ``SDateRange(nullable, from, to)`` (:2188-2250), ``SString.Prefix`` /
+  ``.Suffix`` (:1144-1158), ``SString.DefaultDecodeValue`` (:1131)
 * ``BuildSchema(json)`` — schema/schemabuilder_json.go:124
 
 Extensions needed by the PutAccess / packable mirrors (no reference schema
@@ -36,8 +39,53 @@ __all__ = [
     "SNullFloat32", "SNullFloat64", "SNullUint8", "SNullUint16", "SNullUint32", "SNullUint64",
     "SString", "SStringLen", "SStringExact", "SVariableString", "SBytes", "SVariableBytes",
     "SMap", "SMapSorted", "SVariableMap", "STuple", "STupleVal", "STupleNamed", "STupleNamedVal",
-    "BuildSchema", "TAG_OF_KIND",
+    "SDateRange", "BuildSchema", "TAG_OF_KIND",
+    "CHK_MIN", "CHK_MAX", "CHK_DATE", "CHK_PREFIX", "CHK_SUFFIX", "CHK_DEFAULT",
 ]
+
+# value-check bits (packos_amd/csrc/program.h CHK_*)
+CHK_MIN, CHK_MAX, CHK_DATE, CHK_PREFIX, CHK_SUFFIX, CHK_DEFAULT = 1, 2, 4, 8, 16, 32
+_GO_ZERO_TIME_UNIX = -62135596800   # time.Time{}.Unix()
+
+
+def _unix(t) -> int:
+    """time.Time.Unix() of a datetime (floor), or an int passed through."""
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return t
+    import math
+    return int(math.floor(t.timestamp()))
+
+
+def _rfc3339(sec: int) -> str:
+    import datetime as _dt
+    d = _dt.datetime(1970, 1, 1, tzinfo=_dt.timezone.utc) + _dt.timedelta(seconds=int(sec))
+    return f"{d.year:04d}-{d.month:02d}-{d.day:02d}T{d.hour:02d}:{d.minute:02d}:{d.second:02d}Z"
+
+
+def _parse_rfc3339(txt: str) -> int:
+    """time.Parse(time.RFC3339, txt).Unix(); a parse error gives the zero
+    Time, as BuildSchema discards it (schemabuilder_json.go:169-170)."""
+    import datetime as _dt
+    import re
+    m = re.fullmatch(r"(\d{4})-(\d{2})-(\d{2})T(\d{2}):(\d{2}):(\d{2})(\.\d+)?(Z|[+-]\d{2}:\d{2})", txt or "")
+    if not m:
+        return _GO_ZERO_TIME_UNIX
+    Y, Mo, D, h, mi, sec = (int(m.group(k)) for k in range(1, 7))
+    try:
+        d = _dt.datetime(Y, Mo, D, h, mi, sec, tzinfo=_dt.timezone.utc)
+    except ValueError:
+        return _GO_ZERO_TIME_UNIX
+    tz = m.group(8)
+    off = 0
+    if tz != "Z":
+        th, tm = int(tz[1:3]), int(tz[4:6])
+        if th > 23 or tm > 59:
+            return _GO_ZERO_TIME_UNIX
+        off = (th * 3600 + tm * 60) * (-1 if tz[0] == "-" else 1)
+    epoch = _dt.datetime(1970, 1, 1, tzinfo=_dt.timezone.utc)
+    return int((d - epoch).total_seconds()) - off
 
 # tag written in the header for each node kind (typetags/types.go:6-20)
 TAG_OF_KIND = {
@@ -59,6 +107,9 @@ class Schema:
     names     : TupleSchemaNamed ``FieldNames``
     variable  : TupleSchema ``VariableLength``
     sorted    : map pairs ordered by key bytes (PackMapSorted)
+    check     : CHK_* value checks (Range / SDateRange / Prefix / Suffix /
+                DefaultDecodeValue); rmin / rmax the int bounds, check_lit the
+                prefix or suffix, default the DefaultDecodeVal
     """
 
     kind: str
@@ -69,14 +120,57 @@ class Schema:
     names: Optional[tuple] = None
     variable: bool = False
     sorted: bool = False
+    check: int = 0
+    rmin: int = 0
+    rmax: int = 0
+    check_lit: bytes = b""
+    default: bytes = b""
+
+    # -- value checks (schema/schema.go:1131-1364, 2188-2250) ------------------
+    def Range(self, min=None, max=None) -> "Schema":
+        """SInt16/32/64.Range(min, max): a SchemaGeneric whose precheck is
+        never nullable; out-of-range values fail with ErrOutOfRange on decode
+        and encode (schema.go:1175-1364)."""
+        if self.kind != "int" or self.width not in (2, 4, 8):
+            raise TypeError("Range is defined on SInt16 / SInt32 / SInt64")
+        chk = (CHK_MIN if min is not None else 0) | (CHK_MAX if max is not None else 0)
+        return replace(self, nullable=False, check=chk, rmin=int(min or 0), rmax=int(max or 0))
+
+    def RangeValues(self, min: int, max: int) -> "Schema":
+        return self.Range(min, max)
+
+    def _str_check(self, bit: int, lit) -> "Schema":
+        if self.kind != "string":
+            raise TypeError("Prefix / Suffix are defined on SchemaString")
+        lb = lit.encode() if isinstance(lit, str) else bytes(lit)
+        return replace(self, check=(self.check & CHK_DEFAULT) | bit, check_lit=lb)
+
+    def Prefix(self, prefix) -> "Schema":
+        """SString.Prefix: strings.HasPrefix, ErrStringPrefix (schema.go:1144-1150)."""
+        return self._str_check(CHK_PREFIX, prefix)
+
+    def Suffix(self, suffix) -> "Schema":
+        """SString.Suffix: strings.HasSuffix, ErrStringSuffix (schema.go:1152-1158)."""
+        return self._str_check(CHK_SUFFIX, suffix)
+
+    def DefaultDecodeValue(self, value) -> "Schema":
+        """SchemaString.DefaultDecodeValue: an empty payload decodes as `value`
+        (schema.go:1131-1134, 283-285)."""
+        if self.kind not in ("string", "match"):
+            raise TypeError("DefaultDecodeValue is defined on SchemaString")
+        vb = value.encode() if isinstance(value, str) else bytes(value)
+        chk = (self.check | CHK_DEFAULT) if vb else (self.check & ~CHK_DEFAULT)
+        return replace(self, check=chk, default=vb)
 
     # -- SchemaString helpers (schema/schema.go:1062-1171) ---------------------
     def Match(self, expected) -> "Schema":
         if self.kind != "string":
             raise TypeError("Match is defined on SchemaString")
         lit = expected.encode() if isinstance(expected, str) else bytes(expected)
-        # CheckFunc keeps the receiver's Width as the precheck hint (schema.go:1070-1130)
-        return Schema("match", width=self.width, nullable=self.width <= 0, literal=lit)
+        # CheckFunc keeps the receiver's Width (precheck hint) and its
+        # DefaultDecodeVal (schema.go:1070-1130)
+        return Schema("match", width=self.width, nullable=self.width <= 0, literal=lit,
+                      check=self.check & CHK_DEFAULT, default=self.default)
 
     def WithWidth(self, n: int) -> "Schema":
         if self.kind != "string":
@@ -130,25 +224,41 @@ class Schema:
     # -- SchemaJSON emission (schema/schemabuilder_json.go:8-30) --------------
     def to_json(self) -> dict:
         k = self.kind
+        if k == "int" and self.check & CHK_DATE:
+            d = {"type": "date"}
+            if self.nullable:
+                d["nullable"] = True
+            rng = self.check & (CHK_MIN | CHK_MAX)
+            if rng == (CHK_MIN | CHK_MAX):
+                d["dateFrom"], d["dateTo"] = _rfc3339(self.rmin), _rfc3339(self.rmax)
+            elif rng:
+                raise ValueError("SchemaJSON 'date' takes both dateFrom and dateTo or neither")
+            return d
         if k in ("int", "uint", "float"):
             d = {"type": f"{k}{self.width * 8}"}
             if self.nullable:
                 d["nullable"] = True
+            if self.check & CHK_MIN:
+                d["min"] = self.rmin
+            if self.check & CHK_MAX:
+                d["max"] = self.rmax
             return d
         if k == "bool":
             return {"type": "bool", "nullable": True} if self.nullable else {"type": "bool"}
-        if k == "string":
-            if self.width > 0:
-                return {"type": "string", "width": self.width}
-            if self.width < 0:
-                return {"type": "string", "nullable": True}
-            return {"type": "string"}
-        if k == "match":
-            d = {"type": "string", "exact": self.literal.decode("utf-8")}
+        if k in ("string", "match"):
+            d = {"type": "string"}
             if self.width > 0:
                 d["width"] = self.width
             elif self.width < 0:
                 d["nullable"] = True
+            if self.check & CHK_DEFAULT:
+                d["decodeDefault"] = self.default.decode("utf-8")
+            if k == "match":
+                d["exact"] = self.literal.decode("utf-8")
+            elif self.check & CHK_PREFIX:
+                d["prefix"] = self.check_lit.decode("utf-8")
+            elif self.check & CHK_SUFFIX:
+                d["suffix"] = self.check_lit.decode("utf-8")
             return d
         if k == "bytes":
             return {"type": "bytes", "width": self.width} if self.width > 0 else {"type": "bytes"}
@@ -158,8 +268,6 @@ class Schema:
                 d["fieldNames"] = list(self.names)
             if self.variable:
                 d["variableLength"] = True
-            if not self.nullable:
-                d["nullable"] = False
             return d
         if k == "map":
             d = {"type": "map", "schema": [c.to_json() for c in self.children]}
@@ -167,6 +275,15 @@ class Schema:
                 d["sorted"] = True
             return d
         raise ValueError(k)
+
+
+def SDateRange(nullable: bool, from_=None, to=None) -> "Schema":
+    """SDateRange(nullable, from, to): an int64 Unix-seconds payload checked
+    against [from, to] (datetimes or ints; None = unbounded), failing with
+    ErrDateOutOfRange (schema/schema.go:2188-2250)."""
+    lo, hi = _unix(from_), _unix(to)
+    chk = CHK_DATE | (CHK_MIN if lo is not None else 0) | (CHK_MAX if hi is not None else 0)
+    return Schema("int", width=8, nullable=bool(nullable), check=chk, rmin=lo or 0, rmax=hi or 0)
 
 
 def _scalar(kind, width, nullable=False):
@@ -312,9 +429,15 @@ def BuildSchema(js) -> Schema:
     if t == "bool":
         return SNullBool if nul else SBool
     if t in _INT_W:
-        if js.get("min") is not None or js.get("max") is not None:
-            raise NotImplementedError("Range schemas are outside the compiled subset")
-        return _scalar("int", _INT_W[t], nul)
+        node = _scalar("int", _INT_W[t], nul)
+        lo, hi = js.get("min"), js.get("max")
+        if _INT_W[t] > 1 and (lo is not None or hi is not None):   # int8 ignores them
+            return node.Range(lo, hi)
+        return node
+    if t == "date":
+        if js.get("dateFrom") and js.get("dateTo"):
+            return SDateRange(nul, _parse_rfc3339(js["dateFrom"]), _parse_rfc3339(js["dateTo"]))
+        return SDateRange(nul)
     if t in _UINT_W:
         return _scalar("uint", _UINT_W[t], nul)
     if t in ("float32", "float64"):
@@ -325,11 +448,16 @@ def BuildSchema(js) -> Schema:
             s = s.Optional()
         elif int(js.get("width", 0)) > 0:
             s = s.WithWidth(int(js["width"]))
+        if js.get("decodeDefault"):
+            s = s.DefaultDecodeValue(js["decodeDefault"])
         if js.get("exact"):
             return s.Match(js["exact"])
-        for unsupported in ("prefix", "suffix", "pattern", "decodeDefault"):
-            if js.get(unsupported):
-                raise NotImplementedError(f"string {unsupported} is outside the compiled subset")
+        if js.get("prefix"):
+            return s.Prefix(js["prefix"])
+        if js.get("suffix"):
+            return s.Suffix(js["suffix"])
+        if js.get("pattern"):
+            raise NotImplementedError("string pattern (regexp) is outside the compiled subset")
         return s
     if t == "bytes":
         w = int(js.get("width", 0))
@@ -340,7 +468,8 @@ def BuildSchema(js) -> Schema:
         var = bool(js.get("variableLength", False))
         if js.get("flatten"):
             raise NotImplementedError("flatten/repeat is outside the compiled subset")
-        node = Schema("tuple", nullable=bool(js.get("nullable", True)), children=tuple(kids),
+        # every STuple* is Nullable: true; BuildSchema never reads the key
+        node = Schema("tuple", nullable=True, children=tuple(kids),
                       names=tuple(names) if names else None, variable=var)
         return node
     if t == "map":

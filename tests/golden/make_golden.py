@@ -12,6 +12,11 @@ value, with the same file:line citation.
 
 Cross-API equalities the reference asserts without spelling out bytes
 (e.g. schema.EncodeValue == packable.Pack) are recorded as "equal" groups.
+"inputs" are blobs a reference test builds with pack.Pack(...) without
+spelling out its bytes (the checker's encoder, pinned by the byte vectors
+above, rebuilds them); "decode" cases then name what DecodeBuffer returns
+for them.  Cases marked "derived" restate a reference behaviour no reference
+test exercises (e.g. a Range violation): parity there rests on the cited code.
 
 The reference is Go and no Go toolchain exists in this image, so nothing here
 runs the reference; the JSON is data only.  Run: python tests/golden/make_golden.py
@@ -78,6 +83,8 @@ F32T = {"type": "float32"}
 BOOL = {"type": "bool"}
 STR = {"type": "string"}
 BYT = {"type": "bytes"}
+I16R = {"type": "int16", "min": 0, "max": 20000}      # SInt16.RangeValues(0, 20000)
+I32R = {"type": "int32", "min": 1, "max": 100}        # SInt32.RangeValues(1, 100)
 
 
 def EX(k):
@@ -181,9 +188,28 @@ EQUAL = [
                                            EX("user"), {"type": "bytes", "width": 5}),
                            EX("name"), {"type": "string", "width": 6})]),
         ("packable", [I16, F32T, I64, BOOL,
-                      MAP(EX("meta"), META_SORTED, EX("name"), STR, sorted_=True)])],
+                      MAP(EX("meta"), META_SORTED, EX("name"), STR, sorted_=True)]),
+        # the test's own schema: SInt16.RangeValues(0, 20000) (schema_test.go:1133-1134)
+        ("putaccess", [I16R, F32T, I64, BOOL,
+                       MAP(EX("meta"), MAP(EX("role"), {"type": "bytes", "width": 5},
+                                           EX("user"), {"type": "bytes", "width": 5}),
+                           EX("name"), {"type": "string", "width": 6})])],
      [12345, F32(3.14), 9876543210, True, {"meta": ROW_META, "name": S("gopher")}]),
 ]
+
+# blobs built by pack.Pack(...) inside reference tests (no literal bytes there)
+INPUTS = [
+    ("pack_date_range_email_prefix_suffix", "schema/schema_test.go:407-413 (pack.Pack of five values)", "packable",
+     [STR, I32, STR, STR, STR],
+     [S("2025-09-10"), 42, S("alice@example.com"), S("prefix-hello"), S("world-suffix")]),
+    ("pack_defaults_empty", "schema/schema_test.go:443-450 (pack.Pack with three empty strings)", "packable",
+     [STR, I32, STR, STR, STR], [S("2025-09-10"), 42, S(""), S(""), S("")]),
+]
+
+PACKED_MAP = MAP(EX("meta"), MAP(EX("role"), {"type": "bytes", "width": 5}, EX("user"), {"type": "bytes", "width": 5}),
+                 EX("name"), {"type": "string", "width": 6})
+PACKED_ROW = [12345, F32(3.14), 9876543210, True, {"meta": {"role": B("admin"), "user": B("alice")},
+                                                   "name": S("gopher")}]
 
 # random-access known answers: (pos path, want_tag, want_width, expected payload)
 GET = [
@@ -226,6 +252,41 @@ DECODE = [
                                                EX("user"), {"type": "bytes", "width": 5}),
                                EX("name"), {"type": "string", "width": 6})],
      None, (1 | (5 << 8))),
+    # TestDecodePackedStructure's own schema: SInt16.RangeValues(0, 20000)
+    ("decode_packed_structure_range", "schema/schema_test.go:244-316", "schema_packed_structure",
+     [I16R, F32T, I64, BOOL, PACKED_MAP], PACKED_ROW, 0),
+    # TestDecodeChain_DateEmailPrefixSuffix_Success minus the two Pattern
+    # (regexp) checks, which are outside the compiled subset and pass here
+    ("decode_range_prefix_suffix", "schema/schema_test.go:405-443 (Pattern checks dropped)",
+     "pack_date_range_email_prefix_suffix",
+     [STR, I32R, STR, {"type": "string", "prefix": "prefix-"}, {"type": "string", "suffix": "-suffix"}],
+     [S("2025-09-10"), 42, S("alice@example.com"), S("prefix-hello"), S("world-suffix")], 0),
+    # TestDecodeChain_Default_Success minus the Pattern checks: empty payloads
+    # decode as the DefaultDecodeValue, which then passes Prefix / Suffix
+    ("decode_defaults", "schema/schema_test.go:445-483 (Pattern checks dropped)", "pack_defaults_empty",
+     [STR, I32R, {"type": "string", "decodeDefault": "alice@example.com"},
+      {"type": "string", "decodeDefault": "prefix-hello", "prefix": "prefix-"},
+      {"type": "string", "decodeDefault": "world-suffix", "suffix": "-suffix"}],
+     [S("2025-09-10"), 42, S("alice@example.com"), S("prefix-hello"), S("world-suffix")], 0),
+    # derived (schema.go:1187-1201): 12345 outside RangeValues(0, 10000) ->
+    # ErrOutOfRange at top-level position 0
+    ("derived_range_violation", "derived: schema/schema.go:1187-1201", "schema_packed_structure",
+     [{"type": "int16", "min": 0, "max": 10000}, F32T, I64, BOOL, PACKED_MAP], None, (13 | (1 << 8))),
+    # derived (schema.go:1093-1108, 1144-1150): "prefix-hello" lacks "xyz-" ->
+    # ErrStringPrefix at position 3
+    ("derived_prefix_violation", "derived: schema/schema.go:1093-1108,1144-1150",
+     "pack_date_range_email_prefix_suffix",
+     [STR, I32R, STR, {"type": "string", "prefix": "xyz-"}, STR], None, (6 | (4 << 8))),
+    # derived (schema.go:1152-1158): suffix mismatch -> ErrStringSuffix at 4
+    ("derived_suffix_violation", "derived: schema/schema.go:1152-1158",
+     "pack_date_range_email_prefix_suffix",
+     [STR, I32R, STR, STR, {"type": "string", "suffix": "-nope"}], None, (7 | (5 << 8))),
+    # derived (schema.go:2197-2210, 997-1013): a date (int64, not nullable)
+    # schema over the 4-byte int32 field fails precheck's width test before
+    # any range check: ErrConstraintViolated at position 1
+    ("derived_date_width", "derived: schema/schema.go:2197-2210", "pack_date_range_email_prefix_suffix",
+     [STR, {"type": "date", "dateFrom": "1970-01-01T00:01:00Z", "dateTo": "2000-01-01T00:00:00Z"}, STR, STR, STR],
+     None, (3 | (2 << 8))),
 ]
 
 
@@ -233,7 +294,7 @@ def main():
     if not os.path.isdir(REF):
         sys.exit("reference not present; vectors.json is already committed")
     out = {"note": __doc__.strip().split("\n")[0], "encode": [], "equal": [], "get": [], "seq": [],
-           "decode": []}
+           "inputs": [], "decode": []}
     for cid, src, mode, schema, row, (bf, bl) in ENCODE:
         out["encode"].append({"id": cid, "source": src, "mode": mode, "schema": schema, "row": row,
                               "bytes_from": f"{bf}:{bl}", "hex": extract_bytes(bf, bl).hex()})
@@ -248,13 +309,15 @@ def main():
     for cid, src, (bf, bl) in SEQ:
         out["seq"].append({"id": cid, "source": src, "bytes_from": f"{bf}:{bl}",
                            "hex": extract_bytes(bf, bl).hex()})
+    for cid, src, mode, schema, row in INPUTS:
+        out["inputs"].append({"id": cid, "source": src, "mode": mode, "schema": schema, "row": row})
     for cid, src, from_case, schema, row, status in DECODE:
         out["decode"].append({"id": cid, "source": src, "input_from": from_case, "schema": schema,
                               "expect_row": row, "expect_status": status})
     with open(OUT, "w") as f:
         json.dump(out, f, indent=1)
     print(f"wrote {OUT}: {len(out['encode'])} encode, {len(out['equal'])} equal, "
-          f"{len(out['get'])} get, {len(out['seq'])} seq, {len(out['decode'])} decode")
+          f"{len(out['get'])} get, {len(out['seq'])} seq, {len(out['inputs'])} inputs, {len(out['decode'])} decode")
 
 
 if __name__ == "__main__":

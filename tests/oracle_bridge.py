@@ -28,7 +28,7 @@ class OrSchema(C.Structure):
     _fields_ = [("nodes", C.c_void_p), ("n_nodes", C.c_int), ("n_top", C.c_int),
                 ("lit", C.c_void_p), ("lit_off", C.c_void_p), ("n_cols", C.c_int),
                 ("col_of_node", C.c_int32 * 512), ("next_sibling", C.c_int32 * 512),
-                ("top_nodes", C.c_int32 * 256)]
+                ("top_nodes", C.c_int32 * 256), ("ext", C.c_void_p)]
 
 
 class OrGet(C.Structure):
@@ -99,9 +99,18 @@ class OracleSchema:
     def __init__(self, chain):
         nodes: List[int] = []
         lits: List[bytes] = []
+        ext: List[int] = []
 
         def rec(n):
             k = n.kind
+            li = di = 0
+            if n.check & 0x18:      # prefix / suffix literal
+                li = len(lits) + 1
+                lits.append(n.check_lit)
+            if n.check & 0x20:      # decodeDefault literal
+                di = len(lits) + 1
+                lits.append(n.default)
+            ext.extend([n.check, n.rmin, n.rmax, li | (di << 32)])
             if k == "int":
                 nodes.extend([1, n.width, int(n.nullable), 0])
             elif k == "uint":
@@ -135,7 +144,9 @@ class OracleSchema:
         for l in lits:
             offs.append(offs[-1] + len(l))
         self.lit_off = np.asarray(offs, dtype=np.int32)
+        self.ext = np.asarray(ext, dtype=np.int64)
         s = OrSchema()
+        s.ext = _ptr(self.ext) if any(ext) else None
         s.nodes = _ptr(self.nodes)
         s.n_nodes = len(nodes) // 4
         s.n_top = len(chain.Schemas)

@@ -83,3 +83,96 @@ def rand_value(rng, node: Schema, nil_p=0.15):
 def rand_rows(chain, n, seed, nil_p=0.15):
     rng = random.Random(seed)
     return [[rand_value(rng, s, nil_p) for s in chain.Schemas] for _ in range(n)]
+
+
+# ---- schemas with value checks (Range / SDateRange / Prefix / Suffix / default)
+def rand_checked_leaf(rng, allow_var=True, allow_null=True):
+    from packos_amd.schema import SDateRange
+    r = rng.random()
+    if r < 0.3:
+        base = rng.choice([SInt16, SInt32, SInt64])
+        bits = 8 * base.width
+        lo = rng.randint(-(1 << (bits - 1)), (1 << (bits - 1)) - 1)
+        hi = rng.randint(lo, (1 << (bits - 1)) - 1)
+        which = rng.random()
+        return base.Range(lo if which < 0.7 else None, hi if which > 0.3 else None)
+    if r < 0.45:
+        lo = rng.randint(-60_000_000_000, 200_000_000_000)   # RFC3339 years 68 .. 8300
+        return SDateRange(allow_null and rng.random() < 0.5, lo, lo + rng.randint(0, 1 << 33))
+    if r < 0.75:
+        s = SString if allow_var else SStringLen(rng.randint(1, 6))
+        if allow_var and rng.random() < 0.4:
+            s = s.DefaultDecodeValue(rng.choice(["dflt", "x", "pre-fix", "zz-suf"]))
+        k = rng.random()
+        if k < 0.4:
+            return s.Prefix(rng.choice(["pre", "p", "pre-f"]))
+        if k < 0.8:
+            return s.Suffix(rng.choice(["suf", "f", "-suf"]))
+        return s
+    if r < 0.85 and allow_var:
+        lit = rng.choice(["key", "k"])
+        return SString.DefaultDecodeValue(rng.choice([lit, "other"])).Match(lit)
+    return rand_leaf(rng, allow_var, allow_null)
+
+
+def rand_checked_node(rng, depth, allow_var=True, allow_null=True):
+    r = rng.random()
+    if depth < 2 and r < 0.15:
+        kids = [rand_checked_node(rng, depth + 1, allow_var, allow_null) for _ in range(rng.randint(1, 3))]
+        return STuple(*kids)
+    if depth < 2 and r < 0.25:
+        keys = rng.sample(["alpha", "beta", "gamma", "zz"], rng.randint(1, 2))
+        kids = []
+        for key in keys:
+            kids += [SString.Match(key), rand_checked_node(rng, depth + 1, allow_var, allow_null)]
+        return SMapSorted(*kids)
+    return rand_checked_leaf(rng, allow_var, allow_null)
+
+
+def rand_checked_chain(seed, allow_var=True, allow_null=True, max_top=8):
+    rng = random.Random(seed)
+    return SChain(*[rand_checked_node(rng, 0, allow_var, allow_null) for _ in range(rng.randint(1, max_top))])
+
+
+def _checked_value(rng, node, nil_p):
+    """Values that mostly pass the node's check and sometimes fail it."""
+    from packos_amd.schema import CHK_MAX, CHK_MIN, CHK_PREFIX, CHK_SUFFIX
+    if node.kind == "int" and node.check & (CHK_MIN | CHK_MAX):
+        if node.nullable and rng.random() < nil_p:
+            return None
+        bits = 8 * node.width
+        lo = node.rmin if node.check & CHK_MIN else -(1 << (bits - 1))
+        hi = node.rmax if node.check & CHK_MAX else (1 << (bits - 1)) - 1
+        r = rng.random()
+        if r < 0.9:
+            return rng.randint(lo, hi)
+        if r < 0.95 and lo > -(1 << (bits - 1)):
+            return lo - 1
+        if hi < (1 << (bits - 1)) - 1:
+            return hi + 1
+        return rng.randint(lo, hi)
+    if node.kind == "string" and node.check & (CHK_PREFIX | CHK_SUFFIX):
+        lit = node.check_lit.decode()
+        w = node.width
+        if rng.random() < 0.1:
+            n = w if w > 0 else rng.choice([0, 1, 5])
+            return "".join(rng.choice("abcpf-") for _ in range(n))
+        if w > 0:
+            if len(lit) > w:
+                return "q" * w
+            body = "".join(rng.choice("abcxyz") for _ in range(w - len(lit)))
+        else:
+            body = "".join(rng.choice("abcxyz") for _ in range(rng.choice([0, 2, 9])))
+        return lit + body if node.check & CHK_PREFIX else body + lit
+    if node.kind == "string" and node.width <= 0 and rng.random() < 0.3:
+        return ""   # empty payload: decodes as the default when there is one
+    if node.kind in ("tuple", "map"):
+        if (node.kind == "map" or node.nullable) and rng.random() < nil_p:
+            return None
+        return [_checked_value(rng, ch, nil_p) for ch in node.children]
+    return rand_value(rng, node, nil_p)
+
+
+def rand_checked_rows(chain, n, seed, nil_p=0.15):
+    rng = random.Random(seed)
+    return [[_checked_value(rng, s, nil_p) for s in chain.Schemas] for _ in range(n)]

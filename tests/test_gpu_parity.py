@@ -16,7 +16,7 @@ from packos_amd.api import CompiledSchema, DeviceColumns, decode_batch, encode_b
 from packos_amd.columns import HostColumns
 from packos_amd.configs import CONFIGS, make_columns
 from packos_amd.schema import SBool, SChain, SInt16, SInt32, SInt64, SStringLen, SVariableString, STuple, SMap, SString
-from schema_gen import rand_chain, rand_rows
+from schema_gen import rand_chain, rand_checked_chain, rand_checked_rows, rand_rows
 
 pytestmark = pytest.mark.gpu
 G = load()
@@ -79,7 +79,9 @@ def test_golden_cross_api(case):
     for v in case["variants"]:
         chain = chain_of(v["schema"])
         hc = HostColumns.from_rows(chain, [unwrap(case["row"])])
-        outs.append(bytes(gpu_encode(chain, hc, MODES[v["mode"]])[0]))
+        a, _, st = gpu_encode(chain, hc, MODES[v["mode"]])
+        outs.append(bytes(a))
+        assert int(st[0]) == 0
     assert all(o == outs[0] for o in outs)
 
 
@@ -458,7 +460,7 @@ def assert_same_decode(chain, arena, offs, n, what="", stride=0, gpu=None):
     decodes (status 0).  DecodeBuffer returns (nil, err) on failure
     (schema/schema.go:900-903), so a failing blob's columns are unspecified
     (the fixed-layout fast path may leave tile data in them)."""
-    o_out, o_st = ob.decode(chain, arena, offs, n, nthreads=8)
+    o_out, o_st = ob.decode(chain, arena, offs, n, stride=stride, nthreads=8)
     g_out, g_st = gpu_decode(chain, arena, offs, n, stride) if gpu is None else gpu
     if not np.array_equal(o_st, g_st):
         bad = int(np.nonzero(o_st != g_st)[0][0])
@@ -488,8 +490,12 @@ def assert_same_decode(chain, arena, offs, n, what="", stride=0, gpu=None):
 @pytest.mark.parametrize("case", G["decode"], ids=[c["id"] for c in G["decode"]])
 def test_golden_decode(case):
     src = next((c for c in G["encode"] if c["id"] == case["input_from"]), None)
+    inp = next((c for c in G["inputs"] if c["id"] == case["input_from"]), None)
     if src is not None:
         blob = bytes.fromhex(src["hex"])
+    elif inp is not None:
+        ch = chain_of(inp["schema"])
+        blob = bytes(ob.encode(ch, HostColumns.from_rows(ch, [unwrap(inp["row"])]), MODES[inp["mode"]])[0])
     else:
         eq = next(c for c in G["equal"] if c["id"] == case["input_from"])
         v = eq["variants"][0]
@@ -822,3 +828,59 @@ def _blob_with_nils():
 
 
 from test_oracle_golden import NIL_FIELDS  # noqa: E402
+
+
+# ---------------------------------------------------------- value checks ----
+# Range (SInt*.Range, schema.go:1172-1364), SDateRange (:2188-2250), Prefix /
+# Suffix (:1144-1158), DefaultDecodeValue (:1131, 283-285): the encode status
+# (ErrEncode + top-level field + the leaf's code), decode statuses and default
+# views must match the oracle blob for blob.
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("seed", range(24))
+def test_checked_schema_encode(seed, mode):
+    chain = rand_checked_chain(seed)
+    hc = HostColumns.from_rows(chain, rand_checked_rows(chain, 700, seed + 5))
+    assert_same_encoding(chain, hc, mode, f"checked seed {seed}")
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_checked_schema_encode_fixed(seed):
+    chain = rand_checked_chain(seed, allow_var=False, allow_null=False)
+    hc = HostColumns.from_rows(chain, rand_checked_rows(chain, 3001, seed + 7, nil_p=0.0))
+    assert CompiledSchema(chain).fixed_blob_size > 0
+    assert_same_encoding(chain, hc, 0, f"checked fixed seed {seed}")
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_checked_schema_decode(seed):
+    chain = rand_checked_chain(seed)
+    hc = HostColumns.from_rows(chain, rand_checked_rows(chain, 700, seed + 11))
+    arena, offs, _ = ob.encode(chain, hc, 0)
+    assert_same_decode(chain, arena, offs, hc.n, f"checked seed {seed}")
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_checked_schema_decode_fast(seed):
+    """Fixed layouts with value checks keep the tiled decoder; rows failing a
+    check are re-decoded exactly (status from decode_blob)."""
+    chain = rand_checked_chain(seed, allow_var=False, allow_null=False)
+    assert CompiledSchema(chain).decode_fast
+    hc = HostColumns.from_rows(chain, rand_checked_rows(chain, 3001, seed + 13, nil_p=0.0))
+    arena, offs, _ = ob.encode(chain, hc, 0)
+    B = CompiledSchema(chain).fixed_blob_size
+    assert_same_decode(chain, arena, offs, hc.n, f"checked fast seed {seed}")
+    assert_same_decode(chain, arena, None, hc.n, f"checked fast stride seed {seed}", stride=B)
+
+
+def test_decode_default_views_resolve():
+    """DecodedColumns.var_values resolves PACKOS_VIEW_DEFAULT to the literal."""
+    chain = SChain(SString.DefaultDecodeValue("fallback"), SString)
+    hc = HostColumns.from_rows(chain, [["", "a"], ["xy", ""], ["", ""]])
+    s = CompiledSchema(chain)
+    dc = DeviceColumns.from_host(s, hc, "cuda:0")
+    r = encode_batch(s, dc)
+    out, st = decode_batch(s, r.arena, r.offsets, hc.n)
+    torch().cuda.synchronize()
+    assert st.cpu().tolist() == [0, 0, 0]
+    assert out.var_values(0, r.arena[: r.total]) == [b"fallback", b"xy", b"fallback"]
+    assert out.var_values(1, r.arena[: r.total]) == [b"a", b"", b""]

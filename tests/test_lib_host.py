@@ -39,7 +39,9 @@ def test_schema_errors():
     assert L.packos_schema_compile(b"[{\"type\":\"map\",\"schema\":[{\"type\":\"string\"}]}]", 0,
                                    C.byref(h)) == -2
     assert L.packos_schema_compile(b"[{\"type\":", 0, C.byref(h)) == -2
-    assert L.packos_schema_compile(b"[{\"type\":\"int16\",\"min\":0}]", 0, C.byref(h)) == -3
+    assert L.packos_schema_compile(b"[{\"type\":\"string\",\"pattern\":\"^a\"}]", 0, C.byref(h)) == -3
+    assert L.packos_schema_compile(b"[{\"type\":\"int16\",\"min\":0.5}]", 0, C.byref(h)) == -2
+    assert L.packos_schema_compile(b"[{\"type\":\"uint16\",\"min\":0}]", 0, C.byref(h)) == -3
     assert L.packos_schema_compile(b"[]", 7, C.byref(h)) == -1
 
 
@@ -114,3 +116,29 @@ def test_golden_schemas_compile():
             if hc.valid[c] is not None:
                 valid[c] = hc.valid[c][0]
         assert s.blob_size_host(widths, valid) == len(case["hex"]) // 2, case["id"]
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_checked_schema_bounds_match_compiler(seed):
+    """The compiler's value checks (describe(): min/max/flags in emission
+    order) equal the Python schema tree's, through the SchemaJSON text
+    (RFC3339 dates for SDateRange, int64 min/max for Range)."""
+    from schema_gen import rand_checked_chain
+    chain = rand_checked_chain(seed)
+    got = [tuple(int(kv.split("=")[1]) for kv in l.split()[4:7])
+           for l in CompiledSchema(chain).describe().split("\n") if l.startswith("check ")]
+    want = [(n.check, n.rmin, n.rmax) for n, *_ in chain.walk() if n.check & 0x1B]
+    assert got == want
+
+
+def test_rfc3339_dates():
+    from packos_amd.schema import SDateRange, _parse_rfc3339
+    L = _lib.lib()
+    for txt, unix in [("2025-09-10T00:00:00Z", 1757462400), ("0913-11-12T02:00:13Z", -33328447187),
+                      ("1970-01-01T01:00:00+01:00", 0), ("2000-02-29T12:00:00.75-05:30", 951845400),
+                      ("913-11-12T02:00:13Z", -62135596800), ("2001-02-29T00:00:00Z", -62135596800),
+                      ("bad", -62135596800)]:
+        assert _parse_rfc3339(txt) == unix, txt
+        s = CompiledSchema(json.dumps([{"type": "date", "dateFrom": txt, "dateTo": txt}]))
+        line = next(l for l in s.describe().split("\n") if l.startswith("check "))
+        assert f"min={unix} max={unix}" in line, (txt, line)

@@ -7,6 +7,8 @@ restatement and no GPU parity claim can rest on it.
 import numpy as np
 import pytest
 
+from packos_amd.api import VIEW_DEFAULT
+
 import oracle_bridge as ob
 from golden_util import MODES, chain_of, load, unwrap
 from packos_amd.columns import HostColumns, column_specs
@@ -30,9 +32,10 @@ def test_encode_golden(case):
 
 @pytest.mark.parametrize("case", G["equal"], ids=[c["id"] for c in G["equal"]])
 def test_cross_api_equal(case):
-    outs = [_encode_one(v["schema"], case["row"], MODES[v["mode"]])[0] for v in case["variants"]]
-    for o in outs[1:]:
-        assert o == outs[0], f"{case['id']} ({case['source']})"
+    res = [_encode_one(v["schema"], case["row"], MODES[v["mode"]]) for v in case["variants"]]
+    for o, st in res:
+        assert o == res[0][0], f"{case['id']} ({case['source']})"
+        assert st == 0
 
 
 def test_empty_tuple_bytes():
@@ -151,6 +154,9 @@ def _golden_bytes(case_id):
     for c in G["encode"]:
         if c["id"] == case_id:
             return bytes.fromhex(c["hex"])
+    for c in G["inputs"]:
+        if c["id"] == case_id:
+            return _encode_one(c["schema"], c["row"], MODES[c["mode"]])[0]
     eq = next(c for c in G["equal"] if c["id"] == case_id)
     v = eq["variants"][0]
     return _encode_one(v["schema"], eq["row"], MODES[v["mode"]])[0]
@@ -177,4 +183,5 @@ def test_decode_golden(case):
         if sp.var:
             s0, ln = int(out.start[c][0]), int(out.length[c][0])
             o = exp.offsets[c]
-            assert blob[s0:s0 + ln] == bytes(exp.data[c][o[0]:o[1]])
+            got = sp.node.default[:ln] if s0 == VIEW_DEFAULT else blob[s0:s0 + ln]
+            assert got == bytes(exp.data[c][o[0]:o[1]]), (case["id"], c)
