@@ -276,6 +276,23 @@ int packos_encode_host_batch(const packos_schema* s, const packos_column* host_c
                              uint8_t* host_out, uint64_t out_capacity, uint64_t* host_offsets,
                              uint32_t* host_status, size_t chunk_blobs);
 
+/* Decode n blobs of a HOST arena into HOST columns — the read side of the
+ * cgo shim (BadgerDB values, RPC payloads: DecodeBuffer per blob,
+ * schema/schema.go:893).  Blob i = host_arena[host_offsets[i] ..
+ * host_offsets[i+1]) or, with host_offsets NULL, the `stride`-byte slot i.
+ * Chunks of `chunk_blobs` blobs (0 = 1M) go H2D (their offsets and the arena
+ * bytes they span), through packos_decode_batch, and D2H, on two streams of
+ * the current device so one chunk's copies overlap the other's kernel.
+ * host_cols use packos_decode_batch's layout in host memory; var views are
+ * absolute host_arena offsets (or PACKOS_VIEW_DEFAULT); validity is written
+ * for nullable leaves and containers; rows the decoder does not write (nil
+ * values, leaves inside nil containers) read as zero data and views and 0xFF
+ * validity.  host_status (n) is required.  Pinned
+ * buffers make the copies asynchronous.  Blocks until done.                  */
+int packos_decode_host_batch(const packos_schema* s, const uint8_t* host_arena, const uint64_t* host_offsets,
+                             uint64_t stride, size_t n_blobs, packos_column* host_cols, uint32_t* host_status,
+                             size_t chunk_blobs);
+
 /* ---- batch decode (schema.DecodeBuffer semantics) ------------------------- */
 
 /* blob i = arena[offsets[i] .. offsets[i+1]); offsets == NULL means fixed

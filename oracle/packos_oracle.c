@@ -440,6 +440,27 @@ static void* size_worker(void* arg) {
     return NULL;
 }
 
+/* total encoded bytes of a batch (size pass only), nthreads workers */
+int64_t or_encoded_total(const or_schema* s, const packos_column* cols, size_t n, int mode, uint64_t* offs_scratch,
+                         int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > OR_MAX_THREADS) nthreads = OR_MAX_THREADS;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+    size_job* sj = (size_job*)malloc(sizeof(size_job) * (size_t)nthreads);
+    size_t per = (n + (size_t)nthreads - 1) / (size_t)nthreads;
+    for (int t = 0; t < nthreads; t++) {
+        size_t lo = (size_t)t * per, hi = lo + per > n ? n : lo + per;
+        if (lo > hi) lo = hi;
+        sj[t] = (size_job){s, cols, mode, offs_scratch, lo, hi};
+        pthread_create(&th[t], NULL, size_worker, &sj[t]);
+    }
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    free(th); free(sj);
+    int64_t tot = 0;
+    for (size_t i = 0; i < n; i++) tot += (int64_t)offs_scratch[i + 1];
+    return tot;
+}
+
 int64_t or_encode_batch(const or_schema* s, const packos_column* cols, size_t n, int mode, uint8_t* out,
                         size_t cap, uint64_t* out_offsets, uint32_t* status, int nthreads) {
     if (nthreads < 1) nthreads = 1;

@@ -95,6 +95,9 @@ int64_t or_encode_batch(const or_schema* s, const packos_column* cols, size_t n,
                         uint8_t* out, size_t cap, uint64_t* out_offsets, uint32_t* status,
                         int nthreads);
 int64_t or_encoded_size_one(const or_schema* s, const packos_column* cols, size_t i, int mode);
+/* total bytes of the batch; offs_scratch (n+1) receives per-blob sizes at [1..n] */
+int64_t or_encoded_total(const or_schema* s, const packos_column* cols, size_t n, int mode, uint64_t* offs_scratch,
+                         int nthreads);
 
 /* schema.DecodeBuffer over a batch (host buffers).  offsets n+1 or NULL with
  * stride.  Returns 0.                                                        */

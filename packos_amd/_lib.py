@@ -33,7 +33,7 @@ EXPORTED = [
     "packos_schema_num_top_fields", "packos_schema_column_info", "packos_schema_fixed_blob_size",
     "packos_schema_decode_fast", "packos_schema_column_default",
     "packos_schema_describe", "packos_schema_blob_size_host", "packos_encode_workspace_size",
-    "packos_encoded_size_batch", "packos_encode_batch", "packos_encode_host_batch", "packos_decode_batch",
+    "packos_encoded_size_batch", "packos_encode_batch", "packos_encode_host_batch", "packos_decode_host_batch", "packos_decode_batch",
     "packos_get_field_batch", "packos_get_batch", "packos_strerror", "packos_last_error", "packos_abi_version",
 ]
 
@@ -93,6 +93,7 @@ def lib():
     L.packos_encode_batch.argtypes = [vp, C.POINTER(PackosColumn), sz, vp, u64, vp, vp, vp, sz,
                                       u32, vp]
     L.packos_encode_host_batch.argtypes = [vp, C.POINTER(PackosColumn), sz, vp, u64, vp, vp, sz]
+    L.packos_decode_host_batch.argtypes = [vp, vp, vp, u64, sz, C.POINTER(PackosColumn), vp, sz]
     L.packos_decode_batch.argtypes = [vp, vp, vp, u64, sz, C.POINTER(PackosColumn), vp, vp]
     L.packos_get_field_batch.argtypes = [vp, vp, u64, sz, C.POINTER(C.c_int32), i32, i32, i32,
                                          vp, vp, vp, vp, vp]

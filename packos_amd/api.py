@@ -26,7 +26,8 @@ from ._lib import MODE_PACKABLE, MODE_PUTACCESS, PackosColumn, PackosColumnInfo,
 from .columns import HostColumns, column_specs
 from .schema import SchemaChain
 
-__all__ = ["CompiledSchema", "DeviceColumns", "DecodedColumns", "encode_batch", "decode_batch",
+__all__ = ["CompiledSchema", "DeviceColumns", "DecodedColumns", "HostDecoded", "encode_batch", "decode_batch",
+           "encode_host_batch", "decode_host_batch",
            "get_field_batch", "get_batch", "GET_FIXED", "GET_NULLABLE", "GET_SPAN", "GET_INT",
            "GET_FLOAT", "MODE_PUTACCESS", "MODE_PACKABLE"]
 
@@ -258,6 +259,46 @@ def encode_host_batch(schema: CompiledSchema, hc: HostColumns, chunk_blobs: int 
           "packos_encode_host_batch")
     del keep
     return out[: int(offs[n])], offs, (st[:n] if st is not None else None)
+
+
+class HostDecoded:
+    """Host (numpy) decode output of decode_host_batch, the layout of
+    DecodedColumns: fixed rows, validity, absolute (start, length) views into
+    the host arena."""
+
+    def __init__(self, schema: CompiledSchema, n: int, alloc=np.zeros):
+        self.schema, self.n = schema, n
+        self.data, self.valid, self.start, self.length = [], [], [], []
+        for sp in schema.specs:
+            self.data.append(alloc(max(n * sp.width, 16), np.uint8) if sp.fixed else None)
+            self.valid.append(alloc(max(n, 1), np.uint8) if sp.has_valid else None)
+            self.start.append(alloc(max(n, 1), np.uint64) if sp.var else None)
+            self.length.append(alloc(max(n, 1), np.uint32) if sp.var else None)
+
+    def ctypes_array(self):
+        arr = (PackosColumn * max(1, len(self.schema.specs)))()
+        for c in range(len(self.schema.specs)):
+            for name in ("data", "valid", "start", "length"):
+                a = getattr(self, name)[c]
+                if a is not None:
+                    setattr(arr[c], name, a.ctypes.data)
+        return arr
+
+
+def decode_host_batch(schema: CompiledSchema, arena: np.ndarray, offsets: Optional[np.ndarray], n: int,
+                      stride: int = 0, chunk_blobs: int = 0, out: Optional[HostDecoded] = None,
+                      status: Optional[np.ndarray] = None):
+    """DecodeBuffer over a HOST-resident batch through packos_decode_host_batch
+    (chunked H2D / decode / D2H on two streams; the cgo shim's read entry
+    point).  Returns (HostDecoded, status)."""
+    a = np.ascontiguousarray(arena, dtype=np.uint8)
+    o = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+    out = out if out is not None else HostDecoded(schema, n)
+    st = status if status is not None else np.empty(max(n, 1), np.uint32)
+    check(lib().packos_decode_host_batch(schema.handle, a.ctypes.data if a.size else None,
+                                         None if o is None else o.ctypes.data, stride, n, out.ctypes_array(),
+                                         st.ctypes.data, chunk_blobs), "packos_decode_host_batch")
+    return out, st[:n]
 
 
 class EncodePlan:

@@ -239,3 +239,147 @@ extern "C" int packos_encode_host_batch(const packos_schema* cs, const packos_co
     }
     return PACKOS_OK;
 }
+
+// packos_decode_host_batch: blobs in a HOST arena (BadgerDB values, RPC
+// payloads) decoded into HOST columns.  Chunk k: its offsets (absolute, as
+// the caller's) and the arena bytes they cover (from a 16-B aligned start)
+// go H2D; packos_decode_batch runs on a device arena pointer biased so that
+// absolute offsets land in the chunk buffer, so var views come back as
+// absolute host-arena offsets with no fix-up; columns + status go D2H.  All
+// sizes are known up front, so the host never waits except for slot reuse.
+namespace {
+struct DSlot {
+    hipStream_t st = nullptr;
+    uint8_t* darena = nullptr;
+    uint64_t* doffs = nullptr;
+    uint64_t* hoffs = nullptr;   // pinned staging for stride-mode offsets
+    uint32_t* dstatus = nullptr;
+    std::vector<void*> ddata, dvalid, dstart, dlen;
+    ~DSlot() {
+        if (st) (void)hipStreamSynchronize(st);
+        for (auto* v : {&ddata, &dvalid, &dstart, &dlen})
+            for (void* p : *v)
+                if (p) (void)hipFree(p);
+        if (darena) (void)hipFree(darena);
+        if (doffs) (void)hipFree(doffs);
+        if (dstatus) (void)hipFree(dstatus);
+        if (hoffs) (void)hipHostFree(hoffs);
+        if (st) (void)hipStreamDestroy(st);
+    }
+};
+}  // namespace
+
+extern "C" int packos_decode_host_batch(const packos_schema* cs, const uint8_t* host_arena,
+                                        const uint64_t* host_offsets, uint64_t stride, size_t n,
+                                        packos_column* host_cols, uint32_t* host_status, size_t chunk_blobs) {
+    packos_schema* s = const_cast<packos_schema*>(cs);
+    if (!s || !host_cols || !host_status || (!host_arena && n)) {
+        set_error("packos_decode_host_batch: bad argument");
+        return PACKOS_E_INVALID;
+    }
+    if (n == 0) return PACKOS_OK;
+    if (!host_offsets && stride == 0) { set_error("offsets or stride required"); return PACKOS_E_INVALID; }
+    const size_t ncol = s->col_node.size();
+    std::vector<ColKind> kind(ncol);
+    std::vector<char> has_valid(ncol, 0);   // the decoder writes validity for these
+    for (size_t c = 0; c < ncol; c++) {
+        const Node& nd = s->nodes[s->col_node[c]];
+        const bool scalar = nd.kind >= K_INT && nd.kind <= K_BOOL;
+        const bool str = nd.kind == K_STRING || nd.kind == K_BYTES;
+        kind[c].fixed = scalar || (str && nd.width > 0);
+        kind[c].var = str && nd.width <= 0;
+        kind[c].width = kind[c].fixed ? (uint32_t)nd.width : 0u;
+        has_valid[c] = host_cols[c].valid && ((scalar && nd.nullable) || nd.kind == K_TUPLE || nd.kind == K_MAP);
+        if (kind[c].fixed && !host_cols[c].data) { set_error("host decode column without data"); return PACKOS_E_INVALID; }
+        if (kind[c].var && (!host_cols[c].start || !host_cols[c].length)) {
+            set_error("host decode var column without start/length");
+            return PACKOS_E_INVALID;
+        }
+        if (scalar && nd.nullable && !host_cols[c].valid) {
+            set_error("host decode nullable column without valid");
+            return PACKOS_E_INVALID;
+        }
+    }
+    auto off = [&](size_t i) -> uint64_t { return host_offsets ? host_offsets[i] : (uint64_t)i * stride; };
+    size_t chunk = chunk_blobs ? chunk_blobs : (size_t)1 << 20;
+    chunk = std::min(chunk, n);
+    const size_t nch = (n + chunk - 1) / chunk;
+    uint64_t span_max = 0;   // aligned arena bytes of the largest chunk
+    for (size_t k = 0; k < nch; k++) {
+        const size_t s0 = k * chunk, m = std::min(chunk, n - s0);
+        const uint64_t a = off(s0) & ~15ull, b = std::max(off(s0 + m), off(s0));
+        span_max = std::max(span_max, b - a);
+    }
+    DSlot slot[2];
+    for (DSlot& sl : slot) {
+        HP_TRY(hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking));
+        HP_TRY(hipMalloc((void**)&sl.darena, span_max + 64));
+        HP_TRY(hipMalloc((void**)&sl.doffs, (chunk + 1) * sizeof(uint64_t)));
+        if (!host_offsets) HP_TRY(hipHostMalloc((void**)&sl.hoffs, (chunk + 1) * sizeof(uint64_t), hipHostMallocDefault));
+        HP_TRY(hipMalloc((void**)&sl.dstatus, chunk * sizeof(uint32_t)));
+        sl.ddata.assign(ncol, nullptr);
+        sl.dvalid.assign(ncol, nullptr);
+        sl.dstart.assign(ncol, nullptr);
+        sl.dlen.assign(ncol, nullptr);
+        for (size_t c = 0; c < ncol; c++) {
+            if (kind[c].fixed) HP_TRY(hipMalloc(&sl.ddata[c], std::max<size_t>(16, chunk * kind[c].width)));
+            if (has_valid[c]) HP_TRY(hipMalloc(&sl.dvalid[c], std::max<size_t>(16, chunk)));
+            if (kind[c].var) {
+                HP_TRY(hipMalloc(&sl.dstart[c], chunk * sizeof(uint64_t)));
+                HP_TRY(hipMalloc(&sl.dlen[c], chunk * sizeof(uint32_t)));
+            }
+        }
+    }
+    std::vector<packos_column> dc(ncol);
+    for (size_t k = 0; k < nch; k++) {
+        DSlot& sl = slot[k & 1];
+        if (k >= 2) HP_TRY(hipStreamSynchronize(sl.st));   // slot reuse: chunk k-2 is out
+        const size_t s0 = k * chunk, m = std::min(chunk, n - s0);
+        const uint64_t a = off(s0) & ~15ull, b = std::max(off(s0 + m), off(s0));
+        if (host_offsets) {
+            HP_TRY(hipMemcpyAsync(sl.doffs, host_offsets + s0, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, sl.st));
+        } else {
+            for (size_t x = 0; x <= m; x++) sl.hoffs[x] = (uint64_t)(s0 + x) * stride;
+            HP_TRY(hipMemcpyAsync(sl.doffs, sl.hoffs, (m + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, sl.st));
+        }
+        if (b > a) HP_TRY(hipMemcpyAsync(sl.darena, host_arena + a, b - a, hipMemcpyHostToDevice, sl.st));
+        for (size_t c = 0; c < ncol; c++) {
+            // rows the decoder never writes (nil values, values inside nil
+            // containers) come back as zero data and views, 0xFF validity
+            if (kind[c].fixed) HP_TRY(hipMemsetAsync(sl.ddata[c], 0, m * kind[c].width, sl.st));
+            if (has_valid[c]) HP_TRY(hipMemsetAsync(sl.dvalid[c], 0xFF, m, sl.st));
+            if (kind[c].var) {
+                HP_TRY(hipMemsetAsync(sl.dstart[c], 0, m * sizeof(uint64_t), sl.st));
+                HP_TRY(hipMemsetAsync(sl.dlen[c], 0, m * sizeof(uint32_t), sl.st));
+            }
+            memset(&dc[c], 0, sizeof(dc[c]));
+            dc[c].data = sl.ddata[c];
+            dc[c].valid = (uint8_t*)sl.dvalid[c];
+            dc[c].start = (uint64_t*)sl.dstart[c];
+            dc[c].length = (uint32_t*)sl.dlen[c];
+        }
+        // biased arena: device address of host-arena byte x is darena + (x - a)
+        // (only offsets inside [a, b) are ever dereferenced)
+        const uint8_t* biased = sl.darena - a;
+        int rc = packos_decode_batch(s, biased, sl.doffs, 0, m, dc.data(), sl.dstatus, sl.st);
+        if (rc != PACKOS_OK) return rc;
+        HP_TRY(hipMemcpyAsync(host_status + s0, sl.dstatus, m * sizeof(uint32_t), hipMemcpyDeviceToHost, sl.st));
+        for (size_t c = 0; c < ncol; c++) {
+            if (kind[c].fixed) {
+                const size_t w = kind[c].width;
+                HP_TRY(hipMemcpyAsync((uint8_t*)host_cols[c].data + s0 * w, sl.ddata[c], m * w, hipMemcpyDeviceToHost,
+                                      sl.st));
+            }
+            if (has_valid[c])
+                HP_TRY(hipMemcpyAsync(host_cols[c].valid + s0, sl.dvalid[c], m, hipMemcpyDeviceToHost, sl.st));
+            if (kind[c].var) {
+                HP_TRY(hipMemcpyAsync(host_cols[c].start + s0, sl.dstart[c], m * sizeof(uint64_t),
+                                      hipMemcpyDeviceToHost, sl.st));
+                HP_TRY(hipMemcpyAsync(host_cols[c].length + s0, sl.dlen[c], m * sizeof(uint32_t),
+                                      hipMemcpyDeviceToHost, sl.st));
+            }
+        }
+    }
+    for (DSlot& sl : slot) HP_TRY(hipStreamSynchronize(sl.st));
+    return PACKOS_OK;
+}

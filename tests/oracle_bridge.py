@@ -59,6 +59,9 @@ def lib():
         L.or_encoded_size_one.argtypes = [C.POINTER(OrSchema), C.POINTER(PackosColumn),
                                           C.c_size_t, C.c_int]
         L.or_encoded_size_one.restype = C.c_int64
+        L.or_encoded_total.argtypes = [C.POINTER(OrSchema), C.POINTER(PackosColumn), C.c_size_t, C.c_int,
+                                       C.c_void_p, C.c_int]
+        L.or_encoded_total.restype = C.c_int64
         L.or_decode_batch.argtypes = [C.POINTER(OrSchema), C.c_void_p, C.c_void_p, C.c_uint64,
                                       C.c_size_t, C.POINTER(PackosColumn), C.c_void_p, C.c_int]
         L.or_get_init.argtypes = [C.POINTER(OrGet), C.c_void_p, C.c_int64]
@@ -180,11 +183,9 @@ def encode(chain, hc, mode=MODE_PUTACCESS, nthreads=1):
     keep = []
     cols = make_cols(hc, keep)
     n = hc.n
-    total = 0
-    for i in range(n):
-        total += lib().or_encoded_size_one(C.byref(os_.s), cols, i, mode)
-    arena = np.zeros(max(total, 1), dtype=np.uint8)
     offs = np.zeros(n + 1, dtype=np.uint64)
+    total = lib().or_encoded_total(C.byref(os_.s), cols, n, mode, _ptr(offs), max(nthreads, 8))
+    arena = np.zeros(max(total, 1), dtype=np.uint8)
     st = np.zeros(max(n, 1), dtype=np.uint32)
     r = lib().or_encode_batch(C.byref(os_.s), cols, n, mode, _ptr(arena), arena.size, _ptr(offs),
                               _ptr(st), nthreads)

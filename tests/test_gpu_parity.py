@@ -711,13 +711,58 @@ def test_fixed_decode_fast_matches_generic(name, monkeypatch):
                 assert T.equal(a, b), f"{name} column {c} {name_}"
 
 
-@pytest.mark.parametrize("name,n", [("C3", 30_000), ("C4", 30_000), ("M", 30_000), ("C5", 5000)])
+@pytest.mark.parametrize("name,n", [("C1", 1000), ("C2", 100_003), ("C3", 30_000), ("C4", 30_000), ("M", 30_000),
+                                    ("C5", 5000)])
 def test_config_decode(name, n):
     cfg = CONFIGS[name]
     hc = make_columns(cfg, n=n)
-    arena, offs, _ = ob.encode(cfg.chain, hc, 0, nthreads=8)
+    arena, offs, _ = ob.encode(cfg.chain, hc, cfg.mode, nthreads=8)
     st = assert_same_decode(cfg.chain, arena, offs, n, name)
     assert (st == 0).all()
+
+
+@pytest.mark.parametrize("name,n", [("C1", 1000), ("C2", 20_001), ("C3", 20_001), ("C4", 9_999), ("M", 20_001),
+                                    ("C5", 3000)])
+def test_config_roundtrip(name, n):
+    """encode -> decode -> re-encode on the GPU reproduces the bytes
+    (access/put_test.go:12-42, packable/pack_test.go:99-118 round trips; C1
+    is the reference's 1k-tuple plumbing case at full size)."""
+    T = torch()
+    cfg = CONFIGS[name]
+    hc = make_columns(cfg, n=n)
+    s = CompiledSchema(cfg.chain, cfg.mode)
+    r = encode_batch(s, DeviceColumns.from_host(s, hc, "cuda:0"))
+    offs = r.offsets if r.offsets is not None else T.arange(n + 1, device="cuda:0", dtype=T.int64) * r.blob_size
+    out, st = decode_batch(s, r.arena, offs, n)
+    T.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    arena = r.arena[: r.total].cpu().numpy()
+    back = HostColumns(cfg.chain, n)
+    for c, sp in enumerate(back.specs):
+        if sp.fixed:
+            back.data[c] = out.data[c][: n * sp.width].cpu().numpy().copy()
+        if sp.var:
+            st0 = out.start[c][:n].cpu().numpy().view(np.uint64)
+            ln = out.length[c][:n].cpu().numpy().view(np.uint32).astype(np.int64)
+            o = np.zeros(n + 1, np.int64)
+            np.cumsum(ln, out=o[1:])
+            idx = (np.repeat(st0.astype(np.int64) - o[:-1], ln) + np.arange(o[-1])) if o[-1] else np.zeros(0, np.int64)
+            back.data[c] = arena[idx] if o[-1] else np.zeros(0, np.uint8)
+            back.offsets[c] = o.astype(np.uint32)
+        if sp.has_valid:
+            back.valid[c] = out.valid[c][:n].cpu().numpy().copy()
+    a2, o2, s2 = gpu_encode(cfg.chain, back, cfg.mode)
+    assert np.array_equal(a2, arena)
+    assert np.array_equal(o2, offs.cpu().numpy().astype(np.uint64))
+
+
+def test_full_size_c4_vs_oracle():
+    """Config C4 at its full 4,194,304 blobs (1 GiB of output) against the
+    oracle, byte for byte."""
+    cfg = CONFIGS["C4"]
+    hc = make_columns(cfg, n=cfg.shard)
+    assert hc.n == 4_194_304
+    assert_same_encoding(cfg.chain, hc, cfg.mode, "C4 full")
 
 
 # ------------------------------------------------------------ GetAccess ----
@@ -884,3 +929,64 @@ def test_decode_default_views_resolve():
     assert st.cpu().tolist() == [0, 0, 0]
     assert out.var_values(0, r.arena[: r.total]) == [b"fallback", b"xy", b"fallback"]
     assert out.var_values(1, r.arena[: r.total]) == [b"a", b"", b""]
+
+
+# ------------------------------------------------------ host-resident decode ----
+def _same_host_decode(chain, arena, offs, n, got, g_st, what, stride=0):
+    o_out, o_st = ob.decode(chain, arena, offs, n, stride=stride, nthreads=8)
+    assert np.array_equal(o_st, g_st), what
+    ok = o_st[:n] == 0
+    for c, sp in enumerate(o_out.specs):
+        for name in ("data", "valid", "start", "length"):
+            a = getattr(o_out, name)[c]
+            if a is None:
+                continue
+            b = getattr(got, name)[c]
+            if name == "data":   # rows of nil values: zero on both sides
+                w = sp.width
+                assert np.array_equal(a[: n * w].reshape(n, w)[ok], b[: n * w].reshape(n, w)[ok]), (what, c)
+            else:
+                assert np.array_equal(a[:n][ok], b[:n][ok]), (what, c, name)
+
+
+@pytest.mark.parametrize("name,n,chunk,pinned", [("C3", 20000, 3000, False), ("C3", 20000, 0, True),
+                                                 ("M", 10001, 4096, False), ("M", 10001, 4096, True),
+                                                 ("C5", 3000, 700, False), ("C1", 1000, 0, False),
+                                                 ("C4", 5001, 1024, True), ("C2", 7777, 1000, False)])
+def test_decode_host_batch(name, n, chunk, pinned):
+    """packos_decode_host_batch (host arena -> chunked H2D / decode / D2H ->
+    host columns) vs the oracle: views are absolute host-arena offsets."""
+    from packos_amd.api import decode_host_batch
+    T = torch()
+    cfg = CONFIGS[name]
+    hc = make_columns(cfg, n=n)
+    arena, offs, _ = ob.encode(cfg.chain, hc, cfg.mode, nthreads=8)
+    if pinned:
+        arena = T.from_numpy(np.ascontiguousarray(arena)).pin_memory().numpy()
+    s = CompiledSchema(cfg.chain, cfg.mode)
+    got, st = decode_host_batch(s, arena, offs, n, chunk_blobs=chunk)
+    _same_host_decode(cfg.chain, arena, offs, n, got, st, name)
+    B = s.fixed_blob_size
+    if B > 0:   # fixed stride, no offsets
+        got, st = decode_host_batch(s, arena, None, n, stride=B, chunk_blobs=chunk)
+        _same_host_decode(cfg.chain, arena, None, n, got, st, name + " stride", stride=B)
+
+
+@pytest.mark.parametrize("seed", range(0, 40, 4))
+def test_decode_host_batch_random(seed):
+    """Random schemas, checked schemas and corrupted blobs; offsets that start
+    past 0 at odd positions (chunk arenas staged from a 16-B aligned start)."""
+    from packos_amd.api import decode_host_batch
+    for chain, rows in ((rand_chain(seed), None), (rand_checked_chain(seed), "checked")):
+        rr = rand_checked_rows(chain, 2100, seed + 1) if rows else rand_rows(chain, 2100, seed + 1)
+        hc = HostColumns.from_rows(chain, rr)
+        a0, o0, _ = ob.encode(chain, hc, 0)
+        rng = np.random.default_rng(seed)
+        pad = int(rng.integers(1, 40))
+        arena = np.concatenate([np.full(pad, 0xEE, np.uint8), a0, np.zeros(8, np.uint8)])
+        offs = o0 + pad
+        for k in rng.integers(0, a0.size, size=30):   # corrupt some header bytes
+            arena[pad + int(k)] ^= np.uint8(rng.integers(1, 255))
+        s = CompiledSchema(chain, 0)
+        got, st = decode_host_batch(s, arena, offs, hc.n, chunk_blobs=333)
+        _same_host_decode(chain, arena, offs, hc.n, got, st, f"seed {seed} {rows}")
