@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="M")
-    p.add_argument("--n", type=int, default=0, help="blobs per GPU (default: the config's shard)")
+    p.add_argument("--blobs-per-gpu", type=int, default=0, help="blobs per GPU (default: the config's shard)")
     p.add_argument("--sets", type=int, default=3, help="device copies rotated in the timed loop (cold)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / parity leg")
     p.add_argument("--no-host", action="store_true", help="skip the host-resident library leg")
@@ -160,29 +160,30 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (tests only): every rank on one device, gloo for the
+    # harness barrier / timing all-reduce; the driver's runs use neither
+    if os.environ.get("PACKOS_BENCH_DEVICE") is not None:
+        local = int(os.environ["PACKOS_BENCH_DEVICE"])
+    backend = os.environ.get("PACKOS_BENCH_BACKEND", "nccl")
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from packos_amd.api import CompiledSchema, DeviceColumns, EncodePlan
-    from packos_amd.configs import CONFIGS, algorithmic_bytes, global_blob_sizes, make_columns
-    from packos_amd.shard import plan_shards
+    from packos_amd.configs import CONFIGS, algorithmic_bytes, make_columns
+    from packos_amd.shard import config_shard
 
     cfg = CONFIGS[args.config]
     schema = CompiledSchema(cfg.chain, cfg.mode)
     fixed = schema.fixed_blob_size > 0
-    per_gpu = args.n or cfg.shard
-    n_global = per_gpu * world
-    if fixed:
-        sizes = np.full(n_global, schema.fixed_blob_size, dtype=np.int64)
-    else:
-        sizes = global_blob_sizes(cfg, n_global, schema.all_present_size())
-    shards = plan_shards(sizes, world)
-    lo, hi = shards[rank]
-    del sizes
+    per_gpu = args.blobs_per_gpu or cfg.shard
+    lo, hi, n_global = config_shard(cfg, schema, per_gpu, world, rank)
     n = hi - lo
     hc = make_columns(cfg, n=n, lo=lo)
     stream = torch.cuda.current_stream()
@@ -221,7 +222,7 @@ def main():
         el = time.perf_counter() - t0
         if world > 1:
             dist.barrier()
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            t = torch.tensor([el], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         return el, ev0.elapsed_time(ev1) / steps

@@ -15,7 +15,7 @@ import numpy as np
 
 from .columns import HostColumns
 
-__all__ = ["blob_sizes_host", "plan_shards", "slice_columns", "stitch_offsets"]
+__all__ = ["blob_sizes_host", "plan_shards", "slice_columns", "stitch_offsets", "config_shard"]
 
 
 def blob_sizes_host(schema, hc: HostColumns) -> np.ndarray:
@@ -80,3 +80,20 @@ def stitch_offsets(shard_offsets: Sequence[np.ndarray]) -> np.ndarray:
         parts.append(o[1:] + np.uint64(base))
         base += int(o[-1])
     return np.concatenate(parts)
+
+
+def config_shard(cfg, schema, per_gpu: int, world: int, rank: int) -> Tuple[int, int, int]:
+    """The [lo, hi) blob range rank `rank` encodes when `world` ranks split
+    one global synthetic batch of world x per_gpu blobs of config `cfg`
+    byte-balanced (what bench.py --gpus N runs).  Returns (lo, hi, n_global);
+    the rank then generates exactly its slice with make_columns(cfg, hi - lo,
+    lo=lo)."""
+    from .configs import global_blob_sizes
+    n_global = per_gpu * world
+    B = schema.fixed_blob_size
+    if B > 0:
+        sizes = np.full(n_global, B, dtype=np.int64)
+    else:
+        sizes = global_blob_sizes(cfg, n_global, schema.all_present_size())
+    lo, hi = plan_shards(sizes, world)[rank]
+    return lo, hi, n_global

@@ -79,3 +79,49 @@ def test_plan_shards_properties():
         tot = [int(sizes[lo:hi].sum()) for lo, hi in sh]
         assert max(tot) - min(tot) <= 2 * 4096
     assert plan_shards(np.zeros(0, np.int64), 4) == [(0, 0)] * 4
+
+
+def _cfg_worker(rank, world, port, cfg_name, per_gpu, q):
+    """Exactly bench.py's N>1 data path: config_shard -> make_columns(lo) ->
+    encode this rank's slice; no collective but the harness's gather here."""
+    from packos_amd.shard import config_shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = CONFIGS[cfg_name]
+    schema = CompiledSchema(cfg.chain, cfg.mode)
+    lo, hi, n_global = config_shard(cfg, schema, per_gpu, world, rank)
+    mine = make_columns(cfg, n=hi - lo, lo=lo)
+    arena, offs, st = ob.encode(cfg.chain, mine, cfg.mode)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, (lo, hi, arena.tobytes(), offs.tolist()))
+    if rank == 0:
+        full_arena, full_offs, _ = ob.encode(cfg.chain, make_columns(cfg, n=n_global), cfg.mode)
+        stitched = b"".join(g[2] for g in gathered)
+        offsets = stitch_offsets([np.asarray(g[3], np.uint64) for g in gathered])
+        spans = [(g[0], g[1]) for g in gathered]
+        q.put((stitched == full_arena.tobytes(), np.array_equal(offsets, full_offs), spans,
+               [len(g[2]) for g in gathered], n_global))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg_name,per_gpu,world", [("C5", 1500, 2), ("C3", 2000, 2), ("M", 1024, 2), ("C5", 700, 4)])
+def test_config_shards_like_bench(cfg_name, per_gpu, world):
+    """bench.py --gpus N splits ONE global batch of N x per_gpu blobs by bytes
+    (packos_amd.shard.config_shard) and each rank generates only its slice:
+    the slices must tile the batch and their encodings stitch to the
+    single-shot encoding."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cfg_worker, args=(r, world, port, cfg_name, per_gpu, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    same_bytes, same_offs, spans, bytes_per, n_global = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert same_bytes and same_offs
+    assert spans[0][0] == 0 and spans[-1][1] == n_global
+    assert all(spans[r][1] == spans[r + 1][0] for r in range(world - 1))
+    assert max(bytes_per) - min(bytes_per) <= 4200 * world   # byte-balanced within a blob or so
