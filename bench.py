@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--no-host", action="store_true", help="skip the host-resident library leg")
     p.add_argument("--no-warm", action="store_true", help="skip the warm (single-set) loop, e.g. for PMC passes")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--op", default="encode", choices=["encode", "decode"],
+                   help="decode: time schema.DecodeBuffer over the encoded shard (per-config tables, not the metric)")
     return p.parse_args()
 
 
@@ -146,9 +148,36 @@ def host_leg(schema, hc):
                 best = (el, chunk)
     el, chunk = best
     tot = int(offs[hc.n])
-    return {"million_blobs_per_s": round(hc.n / el / 1e6, 3), "gib_per_s_out": round(tot / el / 2 ** 30, 3),
-            "gib_per_s_in_plus_out": round((tot + hc.nbytes_in()) / el / 2 ** 30, 3),
-            "chunk_blobs": chunk, "note": "pinned host columns -> packos_encode_host_batch -> pinned host arena"}
+    enc = {"million_blobs_per_s": round(hc.n / el / 1e6, 3), "gib_per_s_out": round(tot / el / 2 ** 30, 3),
+           "gib_per_s_in_plus_out": round((tot + hc.nbytes_in()) / el / 2 ** 30, 3),
+           "chunk_blobs": chunk, "note": "pinned host columns -> packos_encode_host_batch -> pinned host arena"}
+    # the read side: the pinned arena just produced -> packos_decode_host_batch
+    # -> pinned host columns (views into the host arena)
+    from packos_amd.api import HostDecoded, decode_host_batch
+
+    def pinned(shape, dtype):
+        return torch.empty(shape, dtype=getattr(torch, np.dtype(dtype).name.replace("uint64", "int64")
+                                                .replace("uint32", "int32"))).pin_memory().numpy().view(dtype)
+    hd = HostDecoded(schema, hc.n, alloc=pinned)
+    hst = pinned(max(hc.n, 1), np.uint32)
+    fixed = schema.fixed_blob_size > 0 and all(v is None for v in hc.valid)
+    dbest = None
+    for chunk in (1 << 18, 1 << 20):
+        for _ in range(2):
+            t0 = time.perf_counter()
+            if fixed:
+                decode_host_batch(schema, out[:tot], None, hc.n, stride=schema.fixed_blob_size, chunk_blobs=chunk,
+                                  out=hd, status=hst)
+            else:
+                decode_host_batch(schema, out[:tot], offs, hc.n, chunk_blobs=chunk, out=hd, status=hst)
+            el = time.perf_counter() - t0
+            if dbest is None or el < dbest[0]:
+                dbest = (el, chunk)
+    ok = bool((hst[:hc.n] == 0).all())
+    enc["decode"] = {"million_blobs_per_s": round(hc.n / dbest[0] / 1e6, 3),
+                     "gib_per_s_in": round(tot / dbest[0] / 2 ** 30, 3), "chunk_blobs": dbest[1], "all_ok": ok,
+                     "note": "pinned host arena -> packos_decode_host_batch -> pinned host columns"}
+    return enc
 
 
 # ----------------------------------------------------------------- main
@@ -202,9 +231,24 @@ def main():
     total_out = sets[0].total
     footprint = sum(p.cols.nbytes() + p.out.numel() for p in sets)
 
+    runs = [p.run for p in sets]
+    if args.op == "decode":
+        from packos_amd.api import DecodedColumns, decode_batch
+        for p in sets:
+            p.run()
+        torch.cuda.synchronize()
+
+        def dec_runner(p):
+            dcols = DecodedColumns(schema, n, dev)
+            st = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+            if fixed:
+                return lambda: decode_batch(schema, p.out, None, n, stride=p.B, stream=stream, out=dcols, status=st)
+            return lambda: decode_batch(schema, p.out, p.offsets, n, stream=stream, out=dcols, status=st)
+        runs = [dec_runner(p) for p in sets]
+
     def timed(plans, steps, warmup):
         for k in range(warmup):
-            plans[k % len(plans)].run()
+            plans[k % len(plans)]()
         torch.cuda.synchronize()
         # HIP events on the launch stream bracket the timed region: elapsed / K
         # is the average step duration on the GPU (a fixed schema's step is the
@@ -216,7 +260,7 @@ def main():
         t0 = time.perf_counter()
         ev0.record(stream)
         for k in range(steps):
-            plans[k % len(plans)].run()
+            plans[k % len(plans)]()
         ev1.record(stream)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
@@ -227,10 +271,19 @@ def main():
             el = float(t.item())
         return el, ev0.elapsed_time(ev1) / steps
 
-    warm_el, warm_kms = (None, None) if args.no_warm else timed(sets[:1], args.steps, args.warmup)
-    el, kernel_ms = timed(sets, args.steps, args.warmup)
+    warm_el, warm_kms = (None, None) if args.no_warm else timed(runs[:1], args.steps, args.warmup)
+    el, kernel_ms = timed(runs, args.steps, args.warmup)
 
     alg = algorithmic_bytes(hc, total_out, with_offsets=not fixed)
+    if args.op == "decode":
+        # DecodeBuffer reads every blob byte except var payloads (returned as
+        # views, never read) + the offsets; writes columns, views, validity, status
+        var_bytes = sum(int(o[-1]) - int(o[0]) for o in hc.offsets if o is not None)
+        out_b = 4 * n
+        for sp in schema.specs:
+            out_b += n * sp.width if sp.fixed else (12 * n if sp.var else 0)
+            out_b += n if sp.has_valid else 0
+        alg = total_out - var_bytes + (0 if fixed else 8 * (n + 1)) + out_b
     blobs = n_global * args.steps
     value = blobs / el / 1e6
     achieved = alg / (kernel_ms * 1e-3) / 1e9
@@ -240,17 +293,20 @@ def main():
     # separate passes of this same command); the summary of such a pass, with
     # its provenance, is read from profiles/ when present.
     traffic, traffic_src = None, None
-    pmc_path = os.path.join(ROOT, "profiles", "r02", f"pmc_{args.config}.json")
+    pmc_name = f"pmc_{args.config}.json" if args.op == "encode" else f"pmc_{args.config}_decode.json"
+    pmc_path = os.path.join(ROOT, "profiles", "r02", pmc_name)
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
                 pmc = json.load(f)
             traffic = pmc.get("hbm_bytes_per_launch")
-            traffic_src = f"profiles/r02/pmc_{args.config}.json: {pmc.get('source', '')}"
+            traffic_src = f"profiles/r02/{pmc_name}: {pmc.get('source', '')}"
         except Exception:
             traffic = None
 
     cpu, parity, host = None, None, None
+    if args.op == "decode":
+        args.no_cpu = args.no_host = True
     if rank == 0 and world == 1 and not args.no_cpu:
         gpu_arena = sets[0].out[:total_out].cpu().numpy()
         gpu_offs = None if fixed else sets[0].offsets.cpu().numpy()
@@ -273,7 +329,8 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "million blobs/s + GiB/s device-resident encode, 1M×256B fixed-schema tuples",
+            "metric": "million blobs/s + GiB/s device-resident encode, 1M×256B fixed-schema tuples"
+                      if args.op == "encode" else "million blobs/s device-resident decode (per-config table)",
             "value": round(value, 3),
             "unit": "million blobs/s",
             "n_gpus": world,
@@ -285,7 +342,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 indexed by global blob, seed 0x%X)" % cfg.seed,
-            "config": {"workload": f"{args.config}: {cfg.note}", "blobs_per_gpu": n, "global_blobs": n_global,
+            "config": {"workload": f"{args.config}: {cfg.note}", "op": args.op, "blobs_per_gpu": n, "global_blobs": n_global,
                        "blob_bytes": schema.fixed_blob_size if fixed else round(total_out / n, 1),
                        "parallelism": f"dp{world} (byte-balanced disjoint shards, no collective)",
                        "sets_rotated": len(sets), "footprint_mib": round(footprint / 2 ** 20, 1)},
