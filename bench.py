@@ -52,8 +52,10 @@ def parse():
     p.add_argument("--no-host", action="store_true", help="skip the host-resident library leg")
     p.add_argument("--no-warm", action="store_true", help="skip the warm (single-set) loop, e.g. for PMC passes")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
-    p.add_argument("--op", default="encode", choices=["encode", "decode"],
-                   help="decode: time schema.DecodeBuffer over the encoded shard (per-config tables, not the metric)")
+    p.add_argument("--op", default="encode", choices=["encode", "decode", "get"],
+                   help="decode: schema.DecodeBuffer over the encoded shard; get: GetAccess GetInt of "
+                        "top-level field --get-pos with the typed gather (per-config tables, not the metric)")
+    p.add_argument("--get-pos", type=int, default=2)
     return p.parse_args()
 
 
@@ -95,6 +97,7 @@ def cpu_leg(cfg, hc, seconds, gpu_arena, gpu_offsets):
     import oracle_bridge as ob  # checker / baseline only
     hi = host_info()
     threads = max(1, min(1024, hi["affinity"] or hi["nproc"]))
+    threads = max(1, min(threads, hc.n // 4096))   # >= 4096 blobs per thread (C1's 1k blobs: one)
     os_ = ob.OracleSchema(cfg.chain)
     keep = []
     cols = ob.make_cols(hc, keep)
@@ -245,6 +248,29 @@ def main():
                 return lambda: decode_batch(schema, p.out, None, n, stride=p.B, stream=stream, out=dcols, status=st)
             return lambda: decode_batch(schema, p.out, p.offsets, n, stream=stream, out=dcols, status=st)
         runs = [dec_runner(p) for p in sets]
+    elif args.op == "get":
+        from packos_amd import _lib
+        import ctypes as C
+        for p in sets:
+            p.run()
+        torch.cuda.synchronize()
+        L = _lib.lib()
+        path = (C.c_int32 * 1)(args.get_pos)
+
+        def get_runner(p):
+            vals = torch.empty((max(n, 1), 8), dtype=torch.uint8, device=dev)
+            s0 = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+            ln = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+            tg = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+            st = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+            offs = None if fixed else p.offsets.data_ptr()
+            stride = p.B if fixed else 0
+            sp = C.c_void_p(stream.cuda_stream)
+            return lambda: L.packos_get_batch(p.out.data_ptr(), offs, stride, n, path, 1, _lib_get_int, 0, 0,
+                                              vals.data_ptr(), 8, s0.data_ptr(), ln.data_ptr(), tg.data_ptr(),
+                                              st.data_ptr(), sp)
+        _lib_get_int = 3   # PACKOS_GET_INT
+        runs = [get_runner(p) for p in sets]
 
     def timed(plans, steps, warmup):
         for k in range(warmup):
@@ -284,6 +310,11 @@ def main():
             out_b += n * sp.width if sp.fixed else (12 * n if sp.var else 0)
             out_b += n if sp.has_valid else 0
         alg = total_out - var_bytes + (0 if fixed else 8 * (n + 1)) + out_b
+    elif args.op == "get":
+        # GetAccess rangeAt: h0 + the two header words around the field + its
+        # payload (8 B for an int64) in; value 8 + start 8 + len 4 + tag 1 +
+        # status 1 out; + the blob offsets for var layouts
+        alg = n * (2 + 4 + 8) + n * 22 + (0 if fixed else 8 * (n + 1))
     blobs = n_global * args.steps
     value = blobs / el / 1e6
     achieved = alg / (kernel_ms * 1e-3) / 1e9
@@ -293,7 +324,7 @@ def main():
     # separate passes of this same command); the summary of such a pass, with
     # its provenance, is read from profiles/ when present.
     traffic, traffic_src = None, None
-    pmc_name = f"pmc_{args.config}.json" if args.op == "encode" else f"pmc_{args.config}_decode.json"
+    pmc_name = f"pmc_{args.config}.json" if args.op == "encode" else f"pmc_{args.config}_{args.op}.json"
     pmc_path = os.path.join(ROOT, "profiles", "r02", pmc_name)
     if os.path.exists(pmc_path):
         try:
@@ -305,7 +336,7 @@ def main():
             traffic = None
 
     cpu, parity, host = None, None, None
-    if args.op == "decode":
+    if args.op != "encode":
         args.no_cpu = args.no_host = True
     if rank == 0 and world == 1 and not args.no_cpu:
         gpu_arena = sets[0].out[:total_out].cpu().numpy()
@@ -330,7 +361,7 @@ def main():
     if rank == 0:
         line = {
             "metric": "million blobs/s + GiB/s device-resident encode, 1M×256B fixed-schema tuples"
-                      if args.op == "encode" else "million blobs/s device-resident decode (per-config table)",
+                      if args.op == "encode" else f"million blobs/s device-resident {args.op} (per-config table)",
             "value": round(value, 3),
             "unit": "million blobs/s",
             "n_gpus": world,
