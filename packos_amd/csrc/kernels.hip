@@ -581,7 +581,6 @@ struct DSeq {
     int next_type, cur_type;
 };
 
-__host__ __device__ __forceinline__ uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
 
 // Byte readers for the decoder: straight from the arena, or from a per-blob
 // LDS window (the blob's first W bytes) with the arena behind it.
@@ -1049,18 +1048,40 @@ struct DGet {
     uint64_t start;
     int64_t len, base, argc;
 };
-__device__ __forceinline__ bool dget_init(DGet& g, const uint8_t* a, uint64_t start, int64_t len) {
+// Byte reader over one blob: its first kGetWin bytes sit in registers (one
+// round of misaligned 16-B loads, whole loads inside the blob only), the rest
+// is read from HBM.  The rangeAt walk of a top-level field then costs one
+// memory round trip instead of three dependent rounds of byte loads.
+constexpr uint32_t kGetWin = 32;
+struct GWin {
+    const uint8_t* a;
+    uint64_t base;
+    uint32_t n;
+    uint32_t W[kGetWin / 4];
+    __device__ __forceinline__ uint32_t byte(uint64_t p) const {
+        const uint64_t d = p - base;
+        if (d < n) {
+            uint32_t w = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < kGetWin / 4; k++) w = (uint32_t)(d >> 2) == k ? W[k] : w;
+            return (w >> (8 * (d & 3))) & 0xFFu;
+        }
+        return a[p];
+    }
+    __device__ __forceinline__ uint32_t u16(uint64_t p) const { return byte(p) | (byte(p + 1) << 8); }
+};
+__device__ __forceinline__ bool dget_init(DGet& g, const GWin& r, uint64_t start, int64_t len) {
     if (len < 2) return false;
-    g.base = rd16(a + start) >> 3;
+    g.base = r.u16(start) >> 3;
     if (len < g.base) return false;
     g.start = start; g.len = len; g.argc = g.base / 2 - 1;
     return true;
 }
 // rangeAt (get.go:38-58)
-__device__ __forceinline__ void dget_range(const DGet& g, const uint8_t* a, int64_t pos, int& tp, int64_t& s,
+__device__ __forceinline__ void dget_range(const DGet& g, const GWin& r, int64_t pos, int& tp, int64_t& s,
                                            int64_t& e) {
     if (pos >= g.argc) { tp = 0; s = -2; e = -1; return; }
-    const uint16_t h1 = rd16(a + g.start + pos * 2), h2 = rd16(a + g.start + (pos + 1) * 2);
+    const uint32_t h1 = r.u16(g.start + pos * 2), h2 = r.u16(g.start + (pos + 1) * 2);
     s = h1 >> 3; tp = h1 & 7;
     e = (h2 >> 3) + g.base;
     if (pos > 0) s += g.base;
@@ -1083,53 +1104,64 @@ __global__ __launch_bounds__(kBlock) void k_get_field(const uint8_t* __restrict_
     if (i >= n) return;
     const uint64_t a0 = offs ? offs[i] : i * stride;
     const uint64_t a1 = offs ? offs[i + 1] : (i + 1) * stride;
+    GWin r;
+    r.a = arena;
+    r.base = a0;
+    const uint64_t bl = a1 > a0 ? a1 - a0 : 0;
+    r.n = bl >= 32 ? 32u : bl >= 16 ? 16u : 0u;
+    {
+        const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+        const u32x4 w0 = r.n >= 16 ? *(const g_u32x4*)(arena + a0) : z;
+        const u32x4 w1 = r.n >= 32 ? *(const g_u32x4*)(arena + a0 + 16) : z;
+        r.W[0] = w0.x; r.W[1] = w0.y; r.W[2] = w0.z; r.W[3] = w0.w;
+        r.W[4] = w1.x; r.W[5] = w1.y; r.W[6] = w1.z; r.W[7] = w1.w;
+    }
     out_start[i] = 0; out_len[i] = 0; out_tag[i] = 0;
     uint8_t* dst = out_values ? out_values + i * value_width : nullptr;
     if (dst)
         for (uint32_t k = 0; k < value_width; k++) dst[k] = 0;
     DGet g;
-    if (!dget_init(g, arena, a0, (int64_t)(a1 - a0))) { status[i] = 3; return; }
+    if (!dget_init(g, r, a0, (int64_t)(a1 - a0))) { status[i] = 3; return; }
     int tp; int64_t s, e;
     for (int d = 0; d < depth - 1; d++) {
-        dget_range(g, arena, path.p[d], tp, s, e);
+        dget_range(g, r, path.p[d], tp, s, e);
         if (e < s || (tp != 7 && tp != 4)) { status[i] = 1; return; }
         if (e == s) { status[i] = 2; return; }
         DGet nx;
-        if (!dget_init(nx, arena, g.start + (uint64_t)s, e - s)) { status[i] = 3; return; }
+        if (!dget_init(nx, r, g.start + (uint64_t)s, e - s)) { status[i] = 3; return; }
         g = nx;
     }
-    dget_range(g, arena, path.p[depth - 1], tp, s, e);
+    dget_range(g, r, path.p[depth - 1], tp, s, e);
     out_tag[i] = (uint8_t)tp;
     const int64_t w = e - s;
-    int r = 0;
+    int rc = 0;
     switch (getter) {
         case PACKOS_GET_NULLABLE:
-            if (w == 0) { r = 4; break; }
+            if (w == 0) { rc = 4; break; }
             [[fallthrough]];
-        case PACKOS_GET_FIXED: r = (tp != want_tag || w != want_width); break;
-        case PACKOS_GET_SPAN: r = (tp != want_tag || e < s); break;
+        case PACKOS_GET_FIXED: rc = (tp != want_tag || w != want_width); break;
+        case PACKOS_GET_SPAN: rc = (tp != want_tag || e < s); break;
         case PACKOS_GET_INT:
-            r = tp != PACKOS_TAG_INTEGER ? 1 : w == 0 ? 4 : (w != 1 && w != 2 && w != 4 && w != 8);
+            rc = tp != PACKOS_TAG_INTEGER ? 1 : w == 0 ? 4 : (w != 1 && w != 2 && w != 4 && w != 8);
             break;
-        case PACKOS_GET_FLOAT: r = tp != PACKOS_TAG_FLOATING ? 1 : w == 0 ? 4 : (w != 4 && w != 8); break;
-        default: r = 1;
+        case PACKOS_GET_FLOAT: rc = tp != PACKOS_TAG_FLOATING ? 1 : w == 0 ? 4 : (w != 4 && w != 8); break;
+        default: rc = 1;
     }
-    status[i] = (uint8_t)r;
-    if (r) return;
+    status[i] = (uint8_t)rc;
+    if (rc) return;
     const uint64_t at = g.start + (uint64_t)s;
     out_start[i] = at;
     out_len[i] = (uint32_t)w;
     if (!dst || getter == PACKOS_GET_SPAN) return;
-    const uint8_t* src = arena + at;
     if (getter == PACKOS_GET_INT) {
         uint64_t v = 0;
-        for (int k = 0; k < w; k++) v |= (uint64_t)src[k] << (8 * k);
+        for (int k = 0; k < w; k++) v |= (uint64_t)r.byte(at + k) << (8 * k);
         if (w < 8 && ((v >> (8 * w - 1)) & 1)) v |= ~0ull << (8 * w);
         for (uint32_t k = 0; k < 8 && k < value_width; k++) dst[k] = (uint8_t)(v >> (8 * k));
     } else if (tp == PACKOS_TAG_BOOL && w == 1) {
-        dst[0] = src[0] != 0;
+        dst[0] = r.byte(at) != 0;
     } else {
-        for (int64_t k = 0; k < w && k < (int64_t)value_width; k++) dst[k] = src[k];
+        for (int64_t k = 0; k < w && k < (int64_t)value_width; k++) dst[k] = (uint8_t)r.byte(at + k);
     }
 }
 
@@ -1536,12 +1568,24 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
         HIP_TRY(hipMemsetAsync(prof[dev], 0, 8 * sizeof(unsigned long long), st));
         V.prof = prof[dev];
 #endif
-        if (V.aff)
-            hipLaunchKernelGGL(k_encode_tiles<true>, dim3((unsigned)ntiles), dim3(kVNT), V.lds_total, st, V,
-                               out_offsets, out, cap, (uint64_t)n, status);
-        else
-            hipLaunchKernelGGL(k_encode_tiles<false>, dim3((unsigned)ntiles), dim3(kVNT), V.lds_total, st, V,
-                               out_offsets, out, cap, (uint64_t)n, status);
+        // instantiated per var-slot bound: the per-blob loops over var slots
+        // (positions, lengths, header offsets) stop at the schema's count
+#define PACKOS_TILES(AFF, NV)                                                                          \
+    hipLaunchKernelGGL((k_encode_tiles<AFF, NV>), dim3((unsigned)ntiles), dim3(kVNT), V.lds_total, st, V, \
+                       out_offsets, out, cap, (uint64_t)n, status)
+        const int nv = V.nvar <= 1 ? 1 : V.nvar <= 2 ? 2 : V.nvar <= 4 ? 4 : 8;
+        if (V.aff) {
+            if (nv == 1) PACKOS_TILES(true, 1);
+            else if (nv == 2) PACKOS_TILES(true, 2);
+            else if (nv == 4) PACKOS_TILES(true, 4);
+            else PACKOS_TILES(true, 8);
+        } else {
+            if (nv == 1) PACKOS_TILES(false, 1);
+            else if (nv == 2) PACKOS_TILES(false, 2);
+            else if (nv == 4) PACKOS_TILES(false, 4);
+            else PACKOS_TILES(false, 8);
+        }
+#undef PACKOS_TILES
         HIP_TRY(hipGetLastError());
 #ifdef PACKOS_PHASE_PROF
         unsigned long long h[8];
