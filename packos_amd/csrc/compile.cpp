@@ -884,6 +884,14 @@ int packos_schema_compile(const char* schema_json, int mode, packos_schema** out
         if ((int)s->col_node.size() > kMaxCols) fail(PACKOS_E_UNSUPPORTED, "more than 64 columns");
         read_tune(s->tune);
         b.build_encode();
+        {   // static prefix read by the decoder's per-blob window
+            int64_t pre = 0;
+            for (const EncItem& it : s->items) {
+                if (it.type == IT_VAR) break;
+                pre += it.size;
+            }
+            s->dec_prefix = pre;
+        }
         b.build_fixed();
         b.build_decode();
         s->dec_fast = canonical_decodes(s) ? 1 : 0;

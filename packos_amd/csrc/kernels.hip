@@ -800,6 +800,9 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
 // load per header word / payload byte with one load round.
 constexpr int kDecWinChunks = 8;
 
+// WC: window chunks per blob — enough for the schema's static prefix (bytes
+// before the first var payload; compile.cpp), at most kDecWinChunks.
+template <int WC>
 __global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols cols, const uint8_t* __restrict__ arena,
                                                        const uint64_t* __restrict__ offs, uint64_t stride, uint64_t n,
                                                        uint32_t* __restrict__ status) {
@@ -845,14 +848,14 @@ __global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols col
     } else {
         w = win + tid * kDecWinChunks * 16;
         b0 = a0 & ~15ull;
-        const uint64_t end = min(a1, b0 + 16ull * kDecWinChunks);
+        const uint64_t end = min(a1, b0 + 16ull * WC);
         const uint32_t nch = (i < n && end > a0) ? (uint32_t)((end - b0 + 15) >> 4) : 0u;
-        u32x4 v[kDecWinChunks];
+        u32x4 v[WC];
 #pragma unroll
-        for (int c = 0; c < kDecWinChunks; c++)
+        for (int c = 0; c < WC; c++)
             if ((uint32_t)c < nch) v[c] = *(const g_u32x4*)(arena + b0 + 16 * c);
 #pragma unroll
-        for (int c = 0; c < kDecWinChunks; c++)
+        for (int c = 0; c < WC; c++)
             if ((uint32_t)c < nch) *(u32x4*)(w + 16 * c) = v[c];
         wbytes = 16 * nch;
     }
@@ -1674,8 +1677,18 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
     } else {
         const size_t ptab = ((s->dnodes.size() * sizeof(DecNode) + 15) & ~(size_t)15) +
                             ((s->dkids.size() * 4 + 15) & ~(size_t)15) + s->lits.size() + 16;
-        hipLaunchKernelGGL(k_decode_win, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), ptab, st, t->dec,
-                           dc, arena, offsets, stride, (uint64_t)n, status);
+        // per-blob window: the static prefix from a 16-B aligned start (+15 B)
+        const int64_t need = (s->dec_prefix + 15 + 15) / 16;
+        const dim3 g((unsigned)((n + kBlock - 1) / kBlock));
+        if (need <= 2)
+            hipLaunchKernelGGL(k_decode_win<2>, g, dim3(kBlock), ptab, st, t->dec, dc, arena, offsets, stride,
+                               (uint64_t)n, status);
+        else if (need <= 4)
+            hipLaunchKernelGGL(k_decode_win<4>, g, dim3(kBlock), ptab, st, t->dec, dc, arena, offsets, stride,
+                               (uint64_t)n, status);
+        else
+            hipLaunchKernelGGL(k_decode_win<kDecWinChunks>, g, dim3(kBlock), ptab, st, t->dec, dc, arena, offsets,
+                               stride, (uint64_t)n, status);
     }
     HIP_TRY(hipGetLastError());
     return PACKOS_OK;
