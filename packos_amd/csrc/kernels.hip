@@ -587,19 +587,43 @@ struct DSeq {
 struct GReader {
     const uint8_t* a;
     __host__ __device__ __forceinline__ uint32_t operator()(uint64_t p) const { return a[p]; }
+    __host__ __device__ __forceinline__ uint32_t u16(uint64_t p) const { return a[p] | (a[p + 1] << 8); }
+    __host__ __device__ __forceinline__ uint32_t u32(uint64_t p) const {
+        return a[p] | (a[p + 1] << 8) | (a[p + 2] << 16) | ((uint32_t)a[p + 3] << 24);
+    }
 };
+// LDS window over arena[base, base + W): dword k of the window at
+// win32[k * stride] (stride 1: one contiguous window; stride kBlock: the
+// per-thread windows interleaved by dword, so the lanes of a wave reading the
+// same window dword hit distinct banks).  Reads of 2 / 4 bytes inside the
+// window are one or two ds_read_b32 + v_alignbyte.
 struct WReader {
     const uint8_t* a;
-    const uint8_t* win;   // LDS copy of arena[base, base + W)
+    const uint32_t* win32;
     uint64_t base;
-    uint32_t W;
+    uint32_t W, stride;
+    __device__ __forceinline__ uint32_t dw(uint32_t k) const { return win32[k * stride]; }
     __device__ __forceinline__ uint32_t operator()(uint64_t p) const {
         const uint64_t d = p - base;
-        return d < W ? win[d] : a[p];
+        return d < W ? (dw((uint32_t)d >> 2) >> (8 * (d & 3))) & 0xFFu : a[p];
+    }
+    __device__ __forceinline__ uint32_t u32(uint64_t p) const {
+        const uint64_t d = p - base;
+        if (d + 4 <= W) {
+            const uint32_t k = (uint32_t)d >> 2, q = (uint32_t)d & 3u;
+            const uint32_t lo = dw(k);
+            return q ? __builtin_amdgcn_alignbyte(dw(k + 1), lo, q) : lo;
+        }
+        return (*this)(p) | ((*this)(p + 1) << 8) | ((*this)(p + 2) << 16) | ((*this)(p + 3) << 24);
+    }
+    __device__ __forceinline__ uint32_t u16(uint64_t p) const {
+        const uint64_t d = p - base;
+        if (d + 2 <= W && (d & 3) != 3) return (dw((uint32_t)d >> 2) >> (8 * (d & 3))) & 0xFFFFu;
+        return (*this)(p) | ((*this)(p + 1) << 8);
     }
 };
 template <class R>
-__host__ __device__ __forceinline__ uint16_t rd16r(const R& r, uint64_t p) { return (uint16_t)(r(p) | (r(p + 1) << 8)); }
+__host__ __device__ __forceinline__ uint16_t rd16r(const R& r, uint64_t p) { return (uint16_t)r.u16(p); }
 
 // NewSeqGetAccess (seqget.go:22-47)
 template <class R>
@@ -645,8 +669,7 @@ constexpr int kPanic = 0x100;
 template <class R>
 __host__ __device__ __forceinline__ void copy_out(uint8_t* dst, const R& r, uint64_t p, uint32_t w) {
     if ((w & 3) == 0 && ((uintptr_t)dst & 3) == 0) {
-        for (uint32_t j = 0; j < w; j += 4)
-            *(uint32_t*)(dst + j) = r(p + j) | (r(p + j + 1) << 8) | (r(p + j + 2) << 16) | (r(p + j + 3) << 24);
+        for (uint32_t j = 0; j < w; j += 4) *(uint32_t*)(dst + j) = r.u32(p + j);
     } else {
         for (uint32_t j = 0; j < w; j++) dst[j] = (uint8_t)r(p + j);
     }
@@ -846,7 +869,8 @@ __global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols col
         b0 = tb;
         wbytes = 16 * nch;
     } else {
-        w = win + tid * kDecWinChunks * 16;
+        // dword k of thread t's window at win32[k * kBlock + t]
+        w = win + 4 * tid;
         b0 = a0 & ~15ull;
         const uint64_t end = min(a1, b0 + 16ull * WC);
         const uint32_t nch = (i < n && end > a0) ? (uint32_t)((end - b0 + 15) >> 4) : 0u;
@@ -854,14 +878,20 @@ __global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols col
 #pragma unroll
         for (int c = 0; c < WC; c++)
             if ((uint32_t)c < nch) v[c] = *(const g_u32x4*)(arena + b0 + 16 * c);
+        uint32_t* w32 = (uint32_t*)w;
 #pragma unroll
         for (int c = 0; c < WC; c++)
-            if ((uint32_t)c < nch) *(u32x4*)(w + 16 * c) = v[c];
+            if ((uint32_t)c < nch) {
+                w32[(4 * c + 0) * kBlock] = v[c].x;
+                w32[(4 * c + 1) * kBlock] = v[c].y;
+                w32[(4 * c + 2) * kBlock] = v[c].z;
+                w32[(4 * c + 3) * kBlock] = v[c].w;
+            }
         wbytes = 16 * nch;
     }
     __syncthreads();
     if (i >= n) return;
-    const WReader R{arena, w, b0, wbytes};
+    const WReader R{arena, (const uint32_t*)w, b0, wbytes, tile_mode ? 1u : (uint32_t)kBlock};
     const DecProgram LP{lnodes, lkids, llits, P.root, P.n_nodes, P.n_kids, P.n_lits};
     status[i] = decode_blob(LP, cols, R, a0, a1, i);
 }
