@@ -816,6 +816,112 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
     return sv;
 }
 
+// Canonical fast path of DecodeBuffer for a flat chain of F leaves: when the
+// blob is exactly F fields + End (h0 = 2(F+1)), every tag matches, offsets
+// rise to End = len, fixed leaves have their width (nullable ones may be
+// empty = nil), MATCH literals and value checks hold, the SeqGetAccess walk
+// (seqget.go:22-103) and every precheck (schema.go:997-1013) succeed and the
+// fields are plain slices: gather them straight from the header words (all
+// read up front).  Anything else returns kFlatFallback and decode_blob runs.
+constexpr uint32_t kFlatFallback = 0xFFFFFFFFu;
+template <class R>
+__device__ __forceinline__ uint32_t decode_flat(const DecProgram& P, const DecCols& cols, const R& r, uint64_t a0,
+                                                uint64_t a1, uint64_t i) {
+    const int F = P.flat;
+    const int64_t len = (int64_t)(a1 - a0);
+    if (len < 4) return kFlatFallback;
+    // header words come from the reader (the LDS window for the prefix)
+    const uint32_t h0 = r.u16(a0), hend = r.u16(a0 + 2 * F);
+    const int64_t base = h0 >> 3;
+    if (base != 2 * (F + 1) || len < base || (hend & 7u) != 0 || (int64_t)(hend >> 3) + base != len)
+        return kFlatFallback;
+    const DecNode root = P.nodes[P.root];
+    // pass 1: structure + value checks (no output written)
+    int64_t prev = base;
+    bool bad = false;
+    uint32_t hj = h0;
+    for (int j = 0; j < F && !bad; j++) {
+        {
+            const uint32_t hn = r.u16(a0 + 2 * (j + 1));
+            const DecNode nd = P.nodes[P.kids[root.kid0 + j]];
+            const int64_t o = j == 0 ? base : (int64_t)(hj >> 3) + base;
+            const int64_t nx = (int64_t)(hn >> 3) + base;
+            bad = (int)(hj & 7u) != nd.tag || o < prev || nx < o;
+            hj = hn;
+            prev = o;
+            const int64_t w = nx - o;
+            const uint64_t pay = a0 + (uint64_t)o;
+            if (!bad) {
+                if (nd.kind == K_INT || nd.kind == K_UINT || nd.kind == K_FLOAT || nd.kind == K_BOOL) {
+                    bad = w != nd.width && !(nd.nullable && w == 0);
+                    if (!bad && (nd.check & CHK_RANGE) && w) {
+                        uint64_t u = 0;
+                        for (int x = 0; x < nd.width; x++) u |= (uint64_t)r(pay + x) << (8 * x);
+                        const int sh = 64 - 8 * nd.width;
+                        const int64_t v = (int64_t)(u << sh) >> sh;
+                        bad = ((nd.check & CHK_MIN) && v < nd.rmin) || ((nd.check & CHK_MAX) && v > nd.rmax);
+                    }
+                } else if (nd.kind == K_STRING || nd.kind == K_BYTES) {
+                    bad = nd.width > 0 && w != nd.width;
+                    if (!bad && (nd.check & CHK_STR)) {
+                        const bool dflt = w == 0 && (nd.check & CHK_DEFAULT) && nd.dlit_len > 0;
+                        const uint32_t L = dflt ? nd.dlit_len : (uint32_t)w, K = nd.lit_len;
+                        bad = L < K;
+                        const uint32_t at = (nd.check & CHK_PREFIX) ? 0u : L - K;
+                        for (uint32_t x = 0; !bad && x < K; x++) {
+                            const uint32_t c = dflt ? P.lits[nd.dlit + at + x] : r(pay + at + x);
+                            bad = c != P.lits[nd.lit + x];
+                        }
+                    }
+                } else if (nd.kind == K_MATCH) {
+                    const bool dflt = w == 0 && (nd.check & CHK_DEFAULT) && nd.dlit_len > 0;
+                    const uint32_t L = dflt ? nd.dlit_len : (uint32_t)w;
+                    bad = L != nd.lit_len;
+                    for (uint32_t x = 0; !bad && x < L; x++)
+                        bad = (dflt ? P.lits[nd.dlit + x] : r(pay + x)) != P.lits[nd.lit + x];
+                } else {
+                    bad = true;
+                }
+            }
+        }
+    }
+    if (bad) return kFlatFallback;
+    // pass 2: the fields
+    hj = h0;
+    for (int j = 0; j < F; j++) {
+        const uint32_t hn = r.u16(a0 + 2 * (j + 1));
+        const DecNode nd = P.nodes[P.kids[root.kid0 + j]];
+        const int64_t o = j == 0 ? base : (int64_t)(hj >> 3) + base;
+        const int64_t w = (int64_t)(hn >> 3) + base - o;
+        hj = hn;
+        const uint64_t pay = a0 + (uint64_t)o;
+        switch (nd.kind) {
+            case K_INT: case K_UINT: case K_FLOAT: case K_BOOL: {
+                if (w == 0) {
+                    if (cols.valid[nd.col]) cols.valid[nd.col][i] = 0;
+                    break;
+                }
+                uint8_t* dstp = cols.data[nd.col] + i * (uint64_t)nd.width;
+                if (nd.kind == K_BOOL) dstp[0] = r(pay) != 0;
+                else copy_out(dstp, r, pay, (uint32_t)nd.width);
+                if (cols.valid[nd.col]) cols.valid[nd.col][i] = 1;
+                break;
+            }
+            case K_STRING: case K_BYTES:
+                if (nd.width > 0) {
+                    copy_out(cols.data[nd.col] + i * (uint64_t)nd.width, r, pay, (uint32_t)nd.width);
+                } else {
+                    const bool dflt = w == 0 && (nd.check & CHK_DEFAULT) && nd.dlit_len > 0;
+                    cols.start[nd.col][i] = dflt ? PACKOS_VIEW_DEFAULT : w == 0 ? 0ull : pay;
+                    cols.length[nd.col][i] = dflt ? nd.dlit_len : (uint32_t)w;
+                }
+                break;
+            default: break;
+        }
+    }
+    return 0;
+}
+
 // Generic decode with a per-blob LDS window: every thread first fetches its
 // blob's first kDecWinChunks x 16 bytes (header block, leading fields) with
 // 16-B loads, all in flight, then runs decode_blob reading the window and
@@ -892,8 +998,11 @@ __global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols col
     __syncthreads();
     if (i >= n) return;
     const WReader R{arena, (const uint32_t*)w, b0, wbytes, tile_mode ? 1u : (uint32_t)kBlock};
-    const DecProgram LP{lnodes, lkids, llits, P.root, P.n_nodes, P.n_kids, P.n_lits};
-    status[i] = decode_blob(LP, cols, R, a0, a1, i);
+    const DecProgram LP{lnodes, lkids, llits, P.root, P.n_nodes, P.n_kids, P.n_lits, P.flat};
+    uint32_t sv = kFlatFallback;
+    if (P.flat) sv = decode_flat(LP, cols, R, a0, a1, i);
+    if (sv == kFlatFallback) sv = decode_blob(LP, cols, R, a0, a1, i);
+    status[i] = sv;
 }
 
 // Fixed-layout decode (the transpose of k_encode_fixed_dw).  A workgroup
@@ -1352,6 +1461,12 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     t.dec.n_nodes = (int32_t)s->dnodes.size();
     t.dec.n_kids = (int32_t)s->dkids.size();
     t.dec.n_lits = (int32_t)s->lits.size();
+    {   // flat chain of <= 15 leaves: the canonical fast path applies
+        const Node& root = s->nodes[0];
+        bool flat = !root.kids.empty() && root.kids.size() <= 15;
+        for (int k : root.kids) flat = flat && s->nodes[k].kind != K_TUPLE && s->nodes[k].kind != K_MAP;
+        t.dec.flat = flat ? (int32_t)root.kids.size() : 0;
+    }
     t.dfix.cols = (const DecFix*)(b + o_dfix);
     t.dfix.chk = (const uint32_t*)(b + o_dchk);
     t.dfix.vchk = (const DecChk*)(b + o_dvchk);

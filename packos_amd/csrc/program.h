@@ -184,6 +184,7 @@ struct DecProgram {
     const uint8_t* lits;
     int32_t root;
     int32_t n_nodes, n_kids, n_lits;   // table sizes (for staging into LDS)
+    int32_t flat;      // F > 0: the chain is F leaves (no tuple / map), F <= 15: canonical fast path
 };
 
 // Fixed-layout decode fast path.  A blob whose length is B and whose
