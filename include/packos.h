@@ -60,6 +60,31 @@ extern "C" {
  * (access/direct_write_nullables.go:10-12, packable/packable_nullables.go:23);
  * PackTuple() with no args writes nothing (packable/pack.go:31).             */
 #define PACKOS_MODE_PACKABLE   1
+/* ADR-001 extended containers, OR-ed into either mode above at
+ * packos_schema_compile.  A FORMAT EXTENSION beyond the reference: PackOS
+ * reserves tag 2 (typetags.TypeExtendedTagContainer, typetags/types.go:11)
+ * and names the ADR (README.md:34) but ships no code, test or wire format for
+ * it, so this build defines one.  Every container whose payload fits 13 bits
+ * (<= 8191 bytes) is written exactly as the reference writes it, so blobs
+ * without a large container are byte-identical to the plain modes.  A
+ * container whose payload exceeds 8191 bytes (the reference would truncate
+ * its End offset, Q1) is written extended instead:
+ *     u16  0x0002            EncodeHeader(0, TypeExtendedTagContainer)
+ *     u16  tag               the container's own tag: 4 tuple (also the
+ *                            top-level chain) / 7 map
+ *     u32  e[0..n]           e[j] = off_j << 3 | tag_j — the 16-bit header
+ *                            rules widened: e[0] off = header bytes
+ *                            4 + 4(n+1), e[j] = field j's start relative to
+ *                            the payload, e[n] = End = payload length
+ *     payload
+ * and the parent entry of a field holding an extended container carries
+ * tag 2.  Offsets reach 2^29 - 1 (512 MiB).  The decoders of a schema
+ * compiled with this bit read such blobs (a top-level blob starting 02 00 is
+ * extended; a tag-2 field must be an extended container of the schema's
+ * kind, else ErrInvalidFormat).  Encode status never carries
+ * PACKOS_STATUS_OVERFLOW13 in this mode.  Packable slack (Q2) still follows
+ * the top-level payload.                                                     */
+#define PACKOS_MODE_EXTENDED   0x100
 
 /* ---- PackOS type tags (typetags/types.go:6-20) ---------------------------- */
 #define PACKOS_TAG_END      0
@@ -193,8 +218,13 @@ int  packos_schema_num_columns(const packos_schema* s);
 int  packos_schema_num_top_fields(const packos_schema* s);
 int  packos_schema_column_info(const packos_schema* s, int col, packos_column_info* out);
 /* Blob size in bytes when the schema has no variable-width leaf and a call
- * passes no validity columns (every nullable present), else -1.              */
+ * passes no validity columns (every nullable present), else -1 (also -1 in
+ * extended mode when that size exceeds 8191: blobs may be extended).       */
 int64_t packos_schema_fixed_blob_size(const packos_schema* s);
+/* Extended mode: the most bytes extended header blocks can add to one blob
+ * (sum over containers with fields of 4 + 2(n+1)); 0 for the plain modes.
+ * Host arenas sized n * (static size + this) + all var bytes always fit.    */
+int64_t packos_schema_ext_overhead(const packos_schema* s);
 /* 1 when packos_decode_batch can use the tiled fixed-layout decoder for this
  * schema (fixed size B, B % 4 == 0, B <= 1024, and the all-present blob
  * decodes cleanly), else 0.  Decided at compile time, without a GPU; results

@@ -304,7 +304,96 @@ static int64_t pk_write(const or_schema* s, const packos_column* cols, size_t i,
     return pos + (int64_t)len;
 }
 
+/* ------------------------------------------------------------------------ */
+/* ADR-001 extended containers (PACKOS_MODE_EXTENDED).  NOT reference code:  */
+/* PackOS reserves tag 2 (typetags/types.go:11) and names the ADR            */
+/* (README.md:34) without a format; this restates the format this build      */
+/* defines (include/packos.h).  Written independently of or_put / pk_write   */
+/* (bottom-up: a container's payload is built first, then its header block   */
+/* in 16-bit or extended form) so the two checks cross-validate: with no     */
+/* payload over 8191 bytes both must give the reference bytes.              */
+/* ------------------------------------------------------------------------ */
+typedef struct xbuf { uint8_t* p; size_t len, cap; } xbuf;
+static void xput(xbuf* b, const void* src, size_t n) {
+    grow(&b->p, &b->cap, b->len + n + 1);
+    if (n) memcpy(b->p + b->len, src, n);
+    b->len += n;
+}
+static void xput16(xbuf* b, uint16_t v) { uint8_t t[2] = {(uint8_t)v, (uint8_t)(v >> 8)}; xput(b, t, 2); }
+static void xput32(xbuf* b, uint32_t v) {
+    uint8_t t[4] = {(uint8_t)v, (uint8_t)(v >> 8), (uint8_t)(v >> 16), (uint8_t)(v >> 24)};
+    xput(b, t, 4);
+}
+static int x_field(const or_schema* s, const packos_column* cols, size_t i, int n, int mode, xbuf* b,
+                   int64_t* slack);
+/* container of nk fields (kids) appended to b; returns 1 when written extended */
+static int x_container(const or_schema* s, const packos_column* cols, size_t i, const int* kids, int nk,
+                       int own_tag, int mode, xbuf* b, int64_t* slack) {
+    if (nk == 0) {
+        if (mode == PACKOS_MODE_PUTACCESS) xput16(b, or_encode_header(2, 0)); /* Q3: 10 00 */
+        return 0;
+    }
+    xbuf pay = {0};
+    int64_t* st = (int64_t*)malloc(sizeof(int64_t) * (size_t)nk);
+    int* tg = (int*)calloc((size_t)nk, sizeof(int));
+    for (int j = 0; j < nk; j++) {
+        st[j] = (int64_t)pay.len;
+        tg[j] = x_field(s, cols, i, kids[j], mode, &pay, slack);
+    }
+    int ext = pay.len > 8191;
+    if (ext) {
+        xput16(b, or_encode_header(0, PACKOS_TAG_EXTENDED));
+        xput16(b, (uint16_t)own_tag);
+        xput32(b, (uint32_t)((4 + 4 * (nk + 1)) << 3) | (uint32_t)tg[0]);
+        for (int j = 1; j < nk; j++) xput32(b, (uint32_t)(st[j] << 3) | (uint32_t)tg[j]);
+        xput32(b, (uint32_t)(pay.len << 3));
+    } else {
+        xput16(b, or_encode_header(2 * (nk + 1), tg[0]));
+        for (int j = 1; j < nk; j++) xput16(b, or_encode_header(st[j], tg[j]));
+        xput16(b, or_encode_end((int64_t)pay.len));
+    }
+    xput(b, pay.p, pay.len);
+    free(pay.p); free(st); free(tg);
+    return ext;
+}
+/* one field appended to b; returns the tag its parent entry carries */
+static int x_field(const or_schema* s, const packos_column* cols, size_t i, int n, int mode, xbuf* b,
+                   int64_t* slack) {
+    int k = NK(s, n);
+    if (is_container(k)) {
+        int nullable = (k == ORN_MAP) ? 1 : NA(s, n);
+        if (nullable && !col_valid(&cols[s->col_of_node[n]], i)) return leaf_tag(k); /* nil: 0 bytes */
+        int kids[256];
+        int nk = children(s, n, kids);
+        return x_container(s, cols, i, kids, nk, leaf_tag(k), mode, b, slack) ? PACKOS_TAG_EXTENDED : leaf_tag(k);
+    }
+    size_t len; int nil; uint8_t tmp[8];
+    const uint8_t* p = leaf_bytes(s, cols, i, n, &len, &nil, tmp);
+    if (nil) { *slack += (int64_t)len; return leaf_tag(k); }   /* packable: ValueSize keeps the width */
+    xput(b, p, len);
+    return leaf_tag(k);
+}
+/* whole blob in extended mode: the chain as a tuple (+ packable slack) */
+static int64_t x_encode(const or_schema* s, const packos_column* cols, size_t i, int mode, xbuf* b) {
+    b->len = 0;
+    int64_t slack = 0;
+    if (mode == PACKOS_MODE_PACKABLE && s->n_top == 0) return 0;   /* Pack() with no args */
+    x_container(s, cols, i, s->top_nodes, s->n_top, PACKOS_TAG_TUPLE, mode, b, &slack);
+    if (mode == PACKOS_MODE_PACKABLE && slack) {
+        grow(&b->p, &b->cap, b->len + (size_t)slack + 1);
+        memset(b->p + b->len, 0, (size_t)slack);
+        b->len += (size_t)slack;
+    }
+    return (int64_t)b->len;
+}
+
 int64_t or_encoded_size_one(const or_schema* s, const packos_column* cols, size_t i, int mode) {
+    if (mode & PACKOS_MODE_EXTENDED) {
+        xbuf b = {0};
+        int64_t r = x_encode(s, cols, i, mode & ~PACKOS_MODE_EXTENDED, &b);
+        free(b.p);
+        return r;
+    }
     if (mode == PACKOS_MODE_PACKABLE) {
         if (s->n_top == 0) return 0;
         int64_t sz = 0;
@@ -358,6 +447,14 @@ typedef struct enc_tls { or_put p; or_put pool[16]; } enc_tls;
 static int64_t encode_one_tls(const or_schema* s, const packos_column* cols, size_t i, int mode,
                               uint8_t* out, size_t cap, int* overflow, enc_tls* t) {
     *overflow = 0;
+    if (mode & PACKOS_MODE_EXTENDED) {
+        xbuf b = {0};
+        int64_t r = x_encode(s, cols, i, mode & ~PACKOS_MODE_EXTENDED, &b);
+        if ((size_t)r > cap) r = -1;
+        else if (r > 0) memcpy(out, b.p, (size_t)r);
+        free(b.p);
+        return r;
+    }
     if (mode == PACKOS_MODE_PACKABLE) {
         /* packable.Pack: buffer of ValueSize() bytes, zero filled (pack.go:59-67) */
         if (s->n_top == 0) return 0;
@@ -503,6 +600,24 @@ int or_seq_init(or_seq* s, const uint8_t* buf, int64_t len) {
     s->base = base; s->count = base / 2; s->pos = 0;
     s->cur_off = base; s->cur_type = h0 & 7;
     s->next_off = (h1 >> 3) + base; s->next_type = h1 & 7;
+    s->xw = 0;
+    return 0;
+}
+static uint32_t rd32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+/* ADR-001 extended container (this build's format, include/packos.h) */
+int or_seq_init_ext(or_seq* s, const uint8_t* buf, int64_t len, int xkind) {
+    if (len < 12 || rd16(buf) != or_encode_header(0, PACKOS_TAG_EXTENDED) || rd16(buf + 2) != xkind) return 1;
+    uint32_t e0 = rd32(buf + 4);
+    int64_t base = e0 >> 3;
+    if (base < 12 || (base & 3) || len < base) return 1;
+    uint32_t e1 = rd32(buf + 8);
+    s->buf = buf; s->len = len;
+    s->base = base; s->count = (base - 4) / 4; s->pos = 0;
+    s->cur_off = base; s->cur_type = e0 & 7;
+    s->next_off = (int64_t)(e1 >> 3) + base; s->next_type = e1 & 7;
+    s->xw = 1;
     return 0;
 }
 int or_seq_peek(const or_seq* s, int* typ, int64_t* width) {
@@ -520,6 +635,13 @@ int or_seq_advance(or_seq* s) {
     s->pos++;
     s->cur_off = s->next_off;
     s->cur_type = s->next_type;
+    if (s->cur_type != 0 && s->xw) {   /* extended: a short buffer is an error, not a panic */
+        if (4 + (s->pos + 1) * 4 + 4 > s->len) return 1;
+        uint32_t h = rd32(s->buf + 4 + (s->pos + 1) * 4);
+        s->next_off = (int64_t)(h >> 3) + s->base;
+        s->next_type = h & 7;
+        return 0;
+    }
     if (s->cur_type != 0) {
         if ((s->pos + 1) * 2 + 2 > s->len) return 2;
         uint16_t h = rd16(s->buf + (s->pos + 1) * 2);
@@ -548,6 +670,7 @@ int or_seq_peek_nested(const or_seq* s, or_seq* nested) {
 /* ------------------------------------------------------------------------ */
 typedef struct dec_ctx {
     const or_schema* s; packos_column* cols; size_t i; uint64_t blob_base;
+    int ext;   /* PACKOS_MODE_EXTENDED: tag-2 fields are extended containers */
 } dec_ctx;
 
 #define DEC_PANIC 0x100
@@ -633,14 +756,20 @@ static int dec_node(dec_ctx* c, int n, or_seq* q, uint64_t sub_base) {
         }
         case ORN_TUPLE: case ORN_MAP: {
             int nul = (k == ORN_MAP) ? 1 : NA(s, n);
-            int e = precheck(q, leaf_tag(k), -1, nul, &w);
+            int xc = c->ext && q->cur_type == PACKOS_TAG_EXTENDED;
+            int e = precheck(q, xc ? PACKOS_TAG_EXTENDED : leaf_tag(k), -1, nul, &w);
             if (e) return e;
             int kids[256];
             int nk = children(s, n, kids);
             if (k == ORN_MAP && (nk % 2) != 0) return 3; /* SizeExact (schema.go:395-403) */
             if (w != 0) {
                 or_seq sub;
-                if (or_seq_peek_nested(q, &sub)) return 1;
+                if (xc) {
+                    if (q->next_off - q->cur_off <= 0 || q->next_off > q->len) return 1;
+                    if (or_seq_init_ext(&sub, q->buf + q->cur_off, q->next_off - q->cur_off, leaf_tag(k))) return 1;
+                } else if (or_seq_peek_nested(q, &sub)) {
+                    return 1;
+                }
                 if (k == ORN_TUPLE && nk > 0 && (sub.count - 1) != nk && !NC(s, n)) return 3;
                 uint64_t nb = sub_base + (uint64_t)q->cur_off;
                 for (int j = 0; j < nk; j++) {
@@ -660,10 +789,14 @@ static int dec_node(dec_ctx* c, int n, or_seq* q, uint64_t sub_base) {
 }
 
 static uint32_t decode_one(const or_schema* s, const uint8_t* blob, int64_t len, uint64_t base,
-                           packos_column* cols, size_t i) {
+                           packos_column* cols, size_t i, int ext) {
     or_seq q;
-    if (or_seq_init(&q, blob, len)) return (uint32_t)PACKOS_ERR_INVALID_FORMAT; /* pos -1 */
-    dec_ctx c = {s, cols, i, base};
+    if (ext && len >= 2 && rd16(blob) == or_encode_header(0, PACKOS_TAG_EXTENDED)) {
+        if (or_seq_init_ext(&q, blob, len, PACKOS_TAG_TUPLE)) return (uint32_t)PACKOS_ERR_INVALID_FORMAT;
+    } else if (or_seq_init(&q, blob, len)) {
+        return (uint32_t)PACKOS_ERR_INVALID_FORMAT; /* pos -1 */
+    }
+    dec_ctx c = {s, cols, i, base, ext};
     for (int t = 0; t < s->n_top; t++) {
         int e = dec_node(&c, s->top_nodes[t], &q, base);
         if (e == DEC_PANIC) return PACKOS_STATUS_PANIC | ((uint32_t)(t + 1) << 8);
@@ -674,19 +807,23 @@ static uint32_t decode_one(const or_schema* s, const uint8_t* blob, int64_t len,
 
 typedef struct dec_job {
     const or_schema* s; const uint8_t* arena; const uint64_t* offs; uint64_t stride;
-    packos_column* cols; uint32_t* status; size_t lo, hi;
+    packos_column* cols; uint32_t* status; size_t lo, hi; int ext;
 } dec_job;
 static void* dec_worker(void* arg) {
     dec_job* j = (dec_job*)arg;
     for (size_t i = j->lo; i < j->hi; i++) {
         uint64_t a = j->offs ? j->offs[i] : i * j->stride;
         uint64_t b = j->offs ? j->offs[i + 1] : (i + 1) * j->stride;
-        j->status[i] = decode_one(j->s, j->arena + a, (int64_t)(b - a), a, j->cols, i);
+        j->status[i] = decode_one(j->s, j->arena + a, (int64_t)(b - a), a, j->cols, i, j->ext);
     }
     return NULL;
 }
 int or_decode_batch(const or_schema* s, const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
                     size_t n, packos_column* cols, uint32_t* status, int nthreads) {
+    return or_decode_batch_mode(s, arena, offsets, stride, n, cols, status, nthreads, 0);
+}
+int or_decode_batch_mode(const or_schema* s, const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
+                         size_t n, packos_column* cols, uint32_t* status, int nthreads, int mode) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > OR_MAX_THREADS) nthreads = OR_MAX_THREADS;
     pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
@@ -695,7 +832,7 @@ int or_decode_batch(const or_schema* s, const uint8_t* arena, const uint64_t* of
     for (int t = 0; t < nthreads; t++) {
         size_t lo = (size_t)t * per, hi = lo + per > n ? n : lo + per;
         if (lo > hi) lo = hi;
-        dj[t] = (dec_job){s, arena, offsets, stride, cols, status, lo, hi};
+        dj[t] = (dec_job){s, arena, offsets, stride, cols, status, lo, hi, (mode & PACKOS_MODE_EXTENDED) != 0};
         pthread_create(&th[t], NULL, dec_worker, &dj[t]);
     }
     for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);

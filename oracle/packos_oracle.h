@@ -85,7 +85,9 @@ typedef struct or_schema {
 
 int or_schema_prepare(or_schema* s);   /* 0 ok */
 
-/* Encode blob i into out (cap bytes).  mode = PACKOS_MODE_*.  Returns size or
+/* Encode blob i into out (cap bytes).  mode = PACKOS_MODE_PUTACCESS /
+ * PACKOS_MODE_PACKABLE, optionally | PACKOS_MODE_EXTENDED (ADR-001 extended
+ * containers: this build's format extension, include/packos.h).  Returns size or
  * -1 if cap too small.  *overflow set when a 13-bit truncation happened.     */
 int64_t or_encode_one(const or_schema* s, const packos_column* cols, size_t i, int mode,
                       uint8_t* out, size_t cap, int* overflow);
@@ -104,6 +106,10 @@ int64_t or_encoded_total(const or_schema* s, const packos_column* cols, size_t n
 int or_decode_batch(const or_schema* s, const uint8_t* arena, const uint64_t* offsets,
                     uint64_t stride, size_t n, packos_column* out_cols, uint32_t* status,
                     int nthreads);
+/* same, mode = PACKOS_MODE_EXTENDED reads ADR-001 extended containers */
+int or_decode_batch_mode(const or_schema* s, const uint8_t* arena, const uint64_t* offsets,
+                         uint64_t stride, size_t n, packos_column* out_cols, uint32_t* status,
+                         int nthreads, int mode);
 
 /* ---- SeqGetAccess restatement (access/seqget.go) ---- */
 typedef struct or_seq {
@@ -111,8 +117,12 @@ typedef struct or_seq {
     int64_t count, base, pos;
     int64_t next_off; int next_type;
     int64_t cur_off;  int cur_type;
+    int xw;                            /* 1: ADR-001 extended container (u32 entries) */
 } or_seq;
 int or_seq_init(or_seq* s, const uint8_t* buf, int64_t len);          /* 0 ok */
+/* extended container of kind xkind (4 tuple / 7 map), PACKOS_MODE_EXTENDED:
+ * 02 00 | kind | u32 entries (include/packos.h); 0 ok                      */
+int or_seq_init_ext(or_seq* s, const uint8_t* buf, int64_t len, int xkind);
 int or_seq_peek(const or_seq* s, int* typ, int64_t* width);            /* 0 ok */
 int or_seq_advance(or_seq* s);                                         /* 0 ok */
 int or_seq_next(or_seq* s, int64_t* start, int64_t* width, int* typ);  /* 0 ok */

@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("PACKOS_LIB") or os.path.join(HERE, "libpackos.so")  #
 
 MODE_PUTACCESS = 0
 MODE_PACKABLE = 1
+MODE_EXTENDED = 0x100   # ADR-001 extended containers (include/packos.h), OR-ed into a mode
 ENC_OFFSETS_READY = 1
 ENC_FORCE_GENERIC = 2
 
@@ -79,6 +80,8 @@ def lib():
     L.packos_schema_column_info.argtypes = [vp, i32, C.POINTER(PackosColumnInfo)]
     L.packos_schema_fixed_blob_size.argtypes = [vp]
     L.packos_schema_fixed_blob_size.restype = i64
+    L.packos_schema_ext_overhead.argtypes = [vp]
+    L.packos_schema_ext_overhead.restype = i64
     L.packos_schema_decode_fast.argtypes = [vp]
     L.packos_schema_decode_fast.restype = C.c_int
     L.packos_schema_column_default.argtypes = [vp, i32, C.c_char_p, sz]

@@ -22,14 +22,14 @@ from typing import List, Optional
 import numpy as np
 
 from . import _lib
-from ._lib import MODE_PACKABLE, MODE_PUTACCESS, PackosColumn, PackosColumnInfo, check, lib
+from ._lib import MODE_EXTENDED, MODE_PACKABLE, MODE_PUTACCESS, PackosColumn, PackosColumnInfo, check, lib
 from .columns import HostColumns, column_specs
 from .schema import SchemaChain
 
 __all__ = ["CompiledSchema", "DeviceColumns", "DecodedColumns", "HostDecoded", "encode_batch", "decode_batch",
            "encode_host_batch", "decode_host_batch",
            "get_field_batch", "get_batch", "GET_FIXED", "GET_NULLABLE", "GET_SPAN", "GET_INT",
-           "GET_FLOAT", "MODE_PUTACCESS", "MODE_PACKABLE"]
+           "GET_FLOAT", "MODE_PUTACCESS", "MODE_PACKABLE", "MODE_EXTENDED"]
 
 
 def _torch():
@@ -192,7 +192,7 @@ def encode_batch(schema: CompiledSchema, cols: DeviceColumns, want_offsets: bool
     st = _stream_ptr(stream)
     arr = cols.ctypes_array()
     status = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if want_status else None
-    fixed = (not cols.has_var()) and not cols.any_valid()
+    fixed = (not cols.has_var()) and not cols.any_valid() and schema.fixed_blob_size >= 0
     if fixed:
         B = schema.all_present_size()
         total = B * n
@@ -226,6 +226,7 @@ def host_batch_bound(schema: CompiledSchema, hc: HostColumns) -> int:
     widths = np.zeros(max(1, ncol), dtype=np.uint32)
     valid = np.ones(max(1, ncol), dtype=np.uint8)
     stat = int(L.packos_schema_blob_size_host(schema.handle, widths.ctypes.data, valid.ctypes.data))
+    stat += int(L.packos_schema_ext_overhead(schema.handle))   # extended header blocks (MODE_EXTENDED)
     var_bytes = sum(int(o[hc.n]) - int(o[0]) for o in hc.offsets if o is not None)
     return max(16, hc.n * max(stat, 0) + var_bytes)
 
@@ -318,7 +319,7 @@ class EncodePlan:
         self.schema, self.cols = schema, cols
         n = cols.n
         dev = cols.data[0].device if cols.data and cols.data[0] is not None else torch.device("cuda")
-        self.fixed = (not cols.has_var()) and not cols.any_valid()
+        self.fixed = (not cols.has_var()) and not cols.any_valid() and schema.fixed_blob_size >= 0
         self._arr = cols.ctypes_array()
         self._stream = stream
         self.status = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if want_status else None

@@ -319,12 +319,16 @@ struct Builder {
         s->items.push_back(hdr);
         s->conts[cont_id].hdr_item = (uint16_t)hdr_item;
         s->conts[cont_id].n_kids = (uint16_t)nk;
-        std::vector<int> kid_start;
+        std::vector<int> kid_start, kid_cont;
         for (int k : n.kids) {
             kid_start.push_back((int)s->items.size());
+            const int k_kind = s->nodes[k].kind;
+            kid_cont.push_back(k_kind == K_TUPLE || k_kind == K_MAP ? (int)s->conts.size() + 1 : 0);
             emit_node(k, cont_id);
         }
         int end_item = (int)s->items.size();
+        s->conts[cont_id].end_item = (uint16_t)end_item;
+        s->conts[cont_id].tag = (uint8_t)(n.kind == K_MAP ? tag_of(K_MAP) : tag_of(K_TUPLE));
         if (nk == 0) {
             if (s->mode == PACKOS_MODE_PUTACCESS) {
                 // BeginX/EndNested (or Pack() of an empty accessor) appends End(0)
@@ -341,6 +345,7 @@ struct Builder {
             h.hdr_item = (uint16_t)hdr_item;
             h.cont = (uint16_t)cont_id;
             h.j = (uint16_t)j;
+            h.child = j < nk ? (uint16_t)kid_cont[j] : (uint16_t)0;
             if (j == 0) {
                 int64_t hs = 2 * (int64_t)(nk + 1);
                 h.relative = 0;
@@ -820,6 +825,32 @@ void read_tune(Tune& t) {
     t.decode_generic = getenv("PACKOS_DECODE_GENERIC") != nullptr;
     if (const char* e = getenv("PACKOS_DEC_TILE_BYTES")) t.dec_tile_bytes = std::min(49152, std::max(1024, atoi(e)));
 }
+
+// Same rule as the device's ext_layout_wave (kernels.hip): containers in
+// reverse pre-order (children before their parent), payload = the sizes of
+// the items between its header item and its end item, so a nested container
+// already written extended counts with its grown header block.
+uint64_t ext_layout_host(const packos_schema* s, std::vector<int64_t>& sz) {
+    uint64_t xm = 0;
+    for (int c = (int)s->conts.size() - 1; c >= 0; c--) {
+        const EncCont& ct = s->conts[c];
+        if (ct.n_kids == 0 || ct.hdr_item >= sz.size()) continue;
+        int64_t pay = 0;
+        for (uint32_t k = ct.hdr_item + 1u; k < ct.end_item; k++) pay += sz[k];
+        if (pay > (int64_t)kExtMaxPayload) {
+            sz[ct.hdr_item] = ext_hdr_bytes(ct.n_kids);
+            if (c < 64) xm |= 1ull << c;
+        }
+    }
+    return xm;
+}
+
+int64_t ext_overhead(const packos_schema* s) {
+    int64_t x = 0;
+    for (const EncCont& ct : s->conts)
+        if (ct.n_kids) x += (int64_t)ext_hdr_bytes(ct.n_kids) - 2 * ((int64_t)ct.n_kids + 1);
+    return x;
+}
 }  // namespace packos
 
 extern "C" {
@@ -843,13 +874,15 @@ const char* packos_strerror(int code) {
 }
 
 int packos_schema_compile(const char* schema_json, int mode, packos_schema** out) {
-    if (!schema_json || !out || (mode != PACKOS_MODE_PUTACCESS && mode != PACKOS_MODE_PACKABLE)) {
+    const int base_mode = mode & ~PACKOS_MODE_EXTENDED;
+    if (!schema_json || !out || (base_mode != PACKOS_MODE_PUTACCESS && base_mode != PACKOS_MODE_PACKABLE)) {
         g_err = "packos_schema_compile: bad argument";
         return PACKOS_E_INVALID;
     }
     *out = nullptr;
     auto* s = new packos_schema();
-    s->mode = mode;
+    s->mode = base_mode;
+    s->ext = (mode & PACKOS_MODE_EXTENDED) != 0;
     try {
         std::string txt(schema_json);
         JVal j = JParser(txt).parse();
@@ -923,7 +956,13 @@ int packos_schema_decode_fast(const packos_schema* s) { return s && s->dec_fast 
 
 int64_t packos_schema_fixed_blob_size(const packos_schema* s) {
     if (!s || s->has_var) return -1;
+    if (s->ext && s->all_present_size > (int64_t)kExtMaxPayload) return -1;   // may hold extended containers
     return s->all_present_size;
+}
+
+int64_t packos_schema_ext_overhead(const packos_schema* s) {
+    if (!s) return -1;
+    return s->ext ? packos::ext_overhead(s) : 0;
 }
 
 int64_t packos_schema_column_default(const packos_schema* s, int col, char* buf, size_t cap) {
@@ -956,17 +995,21 @@ int64_t packos_schema_blob_size_host(const packos_schema* s, const uint32_t* wid
         present[c] = p;
     }
     int64_t tot = 0, slack = 0;
-    for (const EncItem& it : s->items) {
+    std::vector<int64_t> sz(s->items.size(), 0);
+    for (size_t k = 0; k < s->items.size(); k++) {
+        const EncItem& it = s->items[k];
         if (!present[it.cont]) continue;
         switch (it.type) {
-            case IT_HDR: case IT_CONST: tot += it.size; break;
+            case IT_HDR: case IT_CONST: sz[k] = it.size; break;
             case IT_FIXED:
                 if (it.nullable && valid && !valid[it.col]) slack += it.size;
-                else tot += it.size;
+                else sz[k] = it.size;
                 break;
-            case IT_VAR: tot += widths ? widths[it.col] : 0; break;
+            case IT_VAR: sz[k] = widths ? widths[it.col] : 0; break;
         }
     }
+    if (s->ext) packos::ext_layout_host(s, sz);
+    for (int64_t z : sz) tot += z;
     if (s->mode == PACKOS_MODE_PACKABLE) tot += slack;
     return tot;
 }

@@ -93,13 +93,15 @@ extern "C" int packos_encode_host_batch(const packos_schema* cs, const packos_co
         }
         any_valid |= hc[c].valid != nullptr;
     }
-    const bool fixed_size = !s->has_var && !any_valid && s->all_present_size >= 0;
+    const bool fixed_size = !s->has_var && !any_valid && s->all_present_size >= 0 &&
+                            !(s->ext && s->all_present_size > (int64_t)kExtMaxPayload);
     if (!fixed_size && !host_offsets) { set_error("host_offsets required for a variable-size batch"); return PACKOS_E_INVALID; }
     // per-blob byte bound without var values: every non-var item present
     // (a nil only removes bytes; packable slack re-adds at most what it removed)
     uint64_t stat = 0;
     for (const EncItem& it : s->items)
         if (it.type != IT_VAR) stat += it.size;
+    if (s->ext) stat += (uint64_t)ext_overhead(s);   // extended header blocks (ADR-001)
 
     // host var offsets of either width; every chunk's device offsets are
     // chunk-relative uint32 (a chunk's var bytes must stay below 4 GiB), so

@@ -569,6 +569,7 @@ typedef __attribute__((address_space(1))) const uint64_t g_u64;
 typedef __attribute__((address_space(1))) const uint8_t g_u8;
 
 #include "encode_var.inc"
+#include "encode_ext.inc"
 
 // =========================================================================
 // decode: schema.DecodeBuffer, one thread per blob
@@ -579,6 +580,7 @@ struct DSeq {
     int64_t len, base, count, pos, next_off, cur_off;
     uint64_t start;     // absolute arena offset of this (sub)buffer
     int next_type, cur_type;
+    int xw;             // 1: an ADR-001 extended container (u32 entries after a 4-byte lead)
 };
 
 
@@ -625,9 +627,24 @@ struct WReader {
 template <class R>
 __host__ __device__ __forceinline__ uint16_t rd16r(const R& r, uint64_t p) { return (uint16_t)r.u16(p); }
 
-// NewSeqGetAccess (seqget.go:22-47)
+// NewSeqGetAccess (seqget.go:22-47).  xkind != 0 (extended mode only): the
+// buffer must be an extended container of that kind (program.h, ADR-001):
+// the same cursor over u32 entries, count = (base - 4) / 4.
 template <class R>
-__host__ __device__ __forceinline__ int dseq_init(DSeq& s, const R& a, uint64_t start, int64_t len) {
+__host__ __device__ __forceinline__ int dseq_init(DSeq& s, const R& a, uint64_t start, int64_t len, int xkind = 0) {
+    if (xkind) {
+        if (len < 12 || rd16r(a, start) != kExtMarker || (int)rd16r(a, start + 2) != xkind) return 1;
+        const uint32_t e0 = a.u32(start + 4);
+        const int64_t base = e0 >> 3;
+        if (base < 12 || (base & 3) || len < base) return 1;
+        const uint32_t e1 = a.u32(start + 8);
+        s.len = len; s.base = base; s.count = (base - 4) / 4; s.pos = 0; s.start = start;
+        s.cur_off = base; s.cur_type = e0 & 7;
+        s.next_off = (int64_t)(e1 >> 3) + base; s.next_type = e1 & 7;
+        s.xw = 1;
+        return 0;
+    }
+    s.xw = 0;
     if (len < 4) return 1;
     const uint16_t h0 = rd16r(a, start);
     const int64_t base = h0 >> 3;
@@ -646,6 +663,13 @@ __host__ __device__ __forceinline__ int dseq_advance(DSeq& s, const R& a) {
     s.cur_off = s.next_off;
     s.cur_type = s.next_type;
     if (s.cur_type != 0) {
+        if (s.xw) {   // extended: entry pos + 1 after the 4-byte lead; a short buffer is an EOF error
+            if (4 + (s.pos + 1) * 4 + 4 > s.len) return 1;
+            const uint32_t h = a.u32(s.start + 4 + (s.pos + 1) * 4);
+            s.next_off = (int64_t)(h >> 3) + s.base;
+            s.next_type = h & 7;
+            return 0;
+        }
         if ((s.pos + 1) * 2 + 2 > s.len) return 2;
         const uint16_t h = rd16r(a, s.start + (s.pos + 1) * 2);
         s.next_off = (h >> 3) + s.base;
@@ -685,7 +709,9 @@ struct Frame {
 // leaves into the output columns and returns the packed status word.  Host +
 // device: the host runs it once on the canonical blob to qualify a schema for
 // the fixed-layout fast path (same code, so the qualification is exact).
-template <class R>
+// EXT (PACKOS_MODE_EXTENDED): a top-level blob starting 02 00 and every
+// tag-2 field are read as extended containers (program.h).
+template <class R, bool EXT = false>
 __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& cols, const R& arena, uint64_t a0,
                                          uint64_t a1, uint64_t i) {
     // the current frame lives in registers; outer frames are spilled to `stk`
@@ -693,7 +719,8 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
     Frame cur;
     Frame stk[kDecDepth];
     int d = 0;
-    if (dseq_init(cur.q, arena, a0, (int64_t)(a1 - a0)))
+    const int xroot = EXT && a1 - a0 >= 2 && rd16r(arena, a0) == kExtMarker ? PACKOS_TAG_TUPLE : 0;
+    if (dseq_init(cur.q, arena, a0, (int64_t)(a1 - a0), xroot))
         return (uint32_t)PACKOS_ERR_INVALID_FORMAT;  // position -1
     cur.node = P.root;
     cur.k = 0;
@@ -716,7 +743,8 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
         DSeq& q = cur.q;
         int64_t w = 0;
         if (nd.kind == K_TUPLE || nd.kind == K_MAP) {
-            err = dprecheck(q, nd.tag, -1, nd.nullable, w);
+            const bool xc = EXT && q.cur_type == PACKOS_TAG_EXTENDED;   // an extended container field
+            err = dprecheck(q, xc ? PACKOS_TAG_EXTENDED : nd.tag, -1, nd.nullable, w);
             if (err) break;
             if (nd.kind == K_MAP && (nd.nkids & 1)) { err = 3; break; }
             if (w != 0) {
@@ -724,7 +752,10 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
                 if (q.next_off - q.cur_off <= 0 || q.next_off > q.len) { err = 1; break; }
                 if (d + 1 >= kDecDepth) { err = 1; break; }
                 Frame c;
-                if (dseq_init(c.q, arena, q.start + q.cur_off, q.next_off - q.cur_off)) { err = 1; break; }
+                if (dseq_init(c.q, arena, q.start + q.cur_off, q.next_off - q.cur_off, xc ? nd.tag : 0)) {
+                    err = 1;
+                    break;
+                }
                 if (nd.kind == K_TUPLE && nd.nkids > 0 && (c.q.count - 1) != nd.nkids && !nd.variable) {
                     err = 3;
                     break;
@@ -931,7 +962,7 @@ constexpr int kDecWinChunks = 8;
 
 // WC: window chunks per blob — enough for the schema's static prefix (bytes
 // before the first var payload; compile.cpp), at most kDecWinChunks.
-template <int WC>
+template <int WC, bool EXT>
 __global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols cols, const uint8_t* __restrict__ arena,
                                                        const uint64_t* __restrict__ offs, uint64_t stride, uint64_t n,
                                                        uint32_t* __restrict__ status) {
@@ -998,10 +1029,10 @@ __global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols col
     __syncthreads();
     if (i >= n) return;
     const WReader R{arena, (const uint32_t*)w, b0, wbytes, tile_mode ? 1u : (uint32_t)kBlock};
-    const DecProgram LP{lnodes, lkids, llits, P.root, P.n_nodes, P.n_kids, P.n_lits, P.flat};
+    const DecProgram LP{lnodes, lkids, llits, P.root, P.n_nodes, P.n_kids, P.n_lits, P.flat, P.ext};
     uint32_t sv = kFlatFallback;
     if (P.flat) sv = decode_flat(LP, cols, R, a0, a1, i);
-    if (sv == kFlatFallback) sv = decode_blob(LP, cols, R, a0, a1, i);
+    if (sv == kFlatFallback) sv = decode_blob<WReader, EXT>(LP, cols, R, a0, a1, i);
     status[i] = sv;
 }
 
@@ -1030,6 +1061,7 @@ struct DecColsK {
 
 __device__ __forceinline__ uint32_t lds_u8(const uint32_t* lds, uint32_t a) { return (lds[a >> 2] >> (8 * (a & 3))) & 0xFFu; }
 
+template <bool EXT>
 __global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecProgram P, DecCols cols, DecColsK K,
                                                          const uint8_t* __restrict__ arena,
                                                          const uint64_t* __restrict__ offs, uint64_t n,
@@ -1077,7 +1109,8 @@ __global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecPro
     if (!__syncthreads_and(ok)) {
         for (uint32_t j = tid; j < rows; j += kBlock) {
             const uint64_t i = blob0 + j;
-            status[i] = decode_blob(P, cols, GReader{arena}, offs ? offs[i] : i * B, offs ? offs[i + 1] : (i + 1) * B, i);
+            status[i] = decode_blob<GReader, EXT>(P, cols, GReader{arena}, offs ? offs[i] : i * B,
+                                                  offs ? offs[i + 1] : (i + 1) * B, i);
         }
         return;
     }
@@ -1178,7 +1211,9 @@ __global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecPro
     for (uint32_t j = tid; j < rows; j += kBlock) {
         const uint64_t i = blob0 + j;
         uint32_t sv = 0;
-        if (fail[j]) sv = decode_blob(P, cols, GReader{arena}, offs ? offs[i] : i * B, offs ? offs[i + 1] : (i + 1) * B, i);
+        if (fail[j])
+            sv = decode_blob<GReader, EXT>(P, cols, GReader{arena}, offs ? offs[i] : i * B,
+                                           offs ? offs[i + 1] : (i + 1) * B, i);
         status[i] = sv;
     }
 }
@@ -1439,6 +1474,7 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     t.enc.n_conts = (int)s->conts.size();
     t.enc.mode = s->mode;
     t.enc.n_lits = (int)s->lits.size();
+    t.enc.ext = s->ext ? 1 : 0;
     t.fix.segs = (const FixSeg*)(b + o_fsegs);
     t.fix.seg_index = (const uint32_t*)(b + o_fidx);
     t.fix.fcols = (const FixCol*)(b + o_fcols);
@@ -1461,6 +1497,7 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     t.dec.n_nodes = (int32_t)s->dnodes.size();
     t.dec.n_kids = (int32_t)s->dkids.size();
     t.dec.n_lits = (int32_t)s->lits.size();
+    t.dec.ext = s->ext ? 1 : 0;
     {   // flat chain of <= 15 leaves: the canonical fast path applies
         const Node& root = s->nodes[0];
         bool flat = !root.kids.empty() && root.kids.size() <= 15;
@@ -1539,6 +1576,23 @@ static int size_pass(packos_schema* s, DeviceTables* t, const EncCols& ec, size_
         HIP_TRY(hipMemsetAsync(offs, 0, sizeof(uint64_t), st));
         return PACKOS_OK;
     }
+    if (s->ext) {
+        // extended mode: per-blob sizes (k_ext_sizes) then an in-place scan
+        if (!ws || ws_bytes < packos_encode_workspace_size(s, n)) {
+            set_error("workspace too small");
+            return PACKOS_E_WORKSPACE;
+        }
+        const size_t lds = (size_t)kWavesPerBlock * ext_pos_words((int)s->items.size()) * 4;
+        if (lds > 64 * 1024) { set_error("schema has too many items for the LDS budget"); return PACKOS_E_UNSUPPORTED; }
+        const uint64_t ntiles = (n + kSzTile - 1) / kSzTile;
+        HIP_TRY(hipMemsetAsync(ws, 0, (ntiles + 1) * sizeof(uint64_t), st));
+        const unsigned grid = (unsigned)std::min<uint64_t>((n + kWavesPerBlock - 1) / kWavesPerBlock, 256 * 16);
+        hipLaunchKernelGGL(k_ext_sizes, dim3(grid), dim3(kBlock), lds, st, t->enc, ec, offs, (uint64_t)n);
+        hipLaunchKernelGGL(k_scan_inplace, dim3((unsigned)ntiles), dim3(kBlock), 0, st, offs, (uint64_t)n,
+                           (uint64_t*)ws);
+        HIP_TRY(hipGetLastError());
+        return PACKOS_OK;
+    }
     AffPlan A;
     if (affine_layout(s, ec, &A)) {
         const uint64_t per = (uint64_t)kBlock * kAffPer;
@@ -1573,7 +1627,7 @@ int packos_encoded_size_batch(const packos_schema* cs, const packos_column* cols
     bool any_nil;
     if ((r = fill_enc_cols(s, cols, ec, &any_nil))) return r;
     hipStream_t st = (hipStream_t)stream;
-    if (!s->has_var && !any_nil) {
+    if (!s->has_var && !any_nil && !(s->ext && s->all_present_size > (int64_t)kExtMaxPayload)) {
         hipLaunchKernelGGL(k_fill_offsets, dim3((unsigned)((n + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
                            out_offsets, (uint64_t)n, (uint64_t)s->all_present_size);
         HIP_TRY(hipGetLastError());
@@ -1619,7 +1673,9 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
                              uint8_t* out, uint64_t cap, uint64_t* out_offsets, uint32_t* status, void* ws,
                              size_t ws_bytes, uint32_t flags, hipStream_t st) {
     int r;
-    const bool fixed_size = !s->has_var && !any_nil;
+    // extended mode: a fixed schema whose blobs exceed 8191 bytes may hold
+    // extended containers, so it takes the extended path with offsets
+    const bool fixed_size = !s->has_var && !any_nil && !(s->ext && s->all_present_size > (int64_t)kExtMaxPayload);
     if (fixed_size) {
         const uint64_t B = (uint64_t)s->all_present_size;
         if (B * n > cap) { set_error("output arena too small"); return PACKOS_E_CAPACITY; }
@@ -1695,6 +1751,20 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
         set_error(offs_ready ? "PACKOS_ENC_OFFSETS_READY without out_offsets"
                              : "out_offsets required for a variable-size schema");
         return PACKOS_E_INVALID;
+    }
+    if (s->ext) {
+        // ADR-001 extended containers: size pass (unless given), then one
+        // wavefront per blob
+        if (!offs_ready) {
+            if ((r = size_pass(s, t, ec, n, out_offsets, ws, ws_bytes, st))) return r;
+        }
+        const size_t lds = (size_t)kWavesPerBlock * ext_pos_words((int)s->items.size()) * 4;
+        if (lds > 64 * 1024) { set_error("schema has too many items for the LDS budget"); return PACKOS_E_UNSUPPORTED; }
+        const unsigned grid = (unsigned)std::min<uint64_t>((n + kWavesPerBlock - 1) / kWavesPerBlock, 256 * 16);
+        hipLaunchKernelGGL(k_encode_ext, dim3(grid), dim3(kBlock), lds, st, t->enc, ec, (const uint64_t*)out_offsets,
+                           (uint64_t)0, out, cap, (uint64_t)n, status);
+        HIP_TRY(hipGetLastError());
+        return PACKOS_OK;
     }
     // default: k_encode_tiles.  Data-independent presence: the kernel computes
     // (and writes) the out offsets itself, no size pass; otherwise the size pass
@@ -1817,23 +1887,31 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
             K.flags[c] = f.flags;
             K.magic[c] = f.magic;
         }
-        hipLaunchKernelGGL(k_decode_fixed, dim3((unsigned)((n + T - 1) / T)), dim3(kBlock), lds, st, F, t->dec,
-                           dc, K, arena, offsets, (uint64_t)n, status);
+        if (s->ext)
+            hipLaunchKernelGGL(k_decode_fixed<true>, dim3((unsigned)((n + T - 1) / T)), dim3(kBlock), lds, st, F,
+                               t->dec, dc, K, arena, offsets, (uint64_t)n, status);
+        else
+            hipLaunchKernelGGL(k_decode_fixed<false>, dim3((unsigned)((n + T - 1) / T)), dim3(kBlock), lds, st, F,
+                               t->dec, dc, K, arena, offsets, (uint64_t)n, status);
     } else {
         const size_t ptab = ((s->dnodes.size() * sizeof(DecNode) + 15) & ~(size_t)15) +
                             ((s->dkids.size() * 4 + 15) & ~(size_t)15) + s->lits.size() + 16;
         // per-blob window: the static prefix from a 16-B aligned start (+15 B)
         const int64_t need = (s->dec_prefix + 15 + 15) / 16;
         const dim3 g((unsigned)((n + kBlock - 1) / kBlock));
-        if (need <= 2)
-            hipLaunchKernelGGL(k_decode_win<2>, g, dim3(kBlock), ptab, st, t->dec, dc, arena, offsets, stride,
-                               (uint64_t)n, status);
-        else if (need <= 4)
-            hipLaunchKernelGGL(k_decode_win<4>, g, dim3(kBlock), ptab, st, t->dec, dc, arena, offsets, stride,
-                               (uint64_t)n, status);
-        else
-            hipLaunchKernelGGL(k_decode_win<kDecWinChunks>, g, dim3(kBlock), ptab, st, t->dec, dc, arena, offsets,
-                               stride, (uint64_t)n, status);
+#define PACKOS_DECWIN(WC, X)                                                                             \
+    hipLaunchKernelGGL((k_decode_win<WC, X>), g, dim3(kBlock), ptab, st, t->dec, dc, arena, offsets, stride, \
+                       (uint64_t)n, status)
+        if (s->ext) {   // extended containers: bigger blobs, no window sizing games
+            PACKOS_DECWIN(kDecWinChunks, true);
+        } else if (need <= 2) {
+            PACKOS_DECWIN(2, false);
+        } else if (need <= 4) {
+            PACKOS_DECWIN(4, false);
+        } else {
+            PACKOS_DECWIN(kDecWinChunks, false);
+        }
+#undef PACKOS_DECWIN
     }
     HIP_TRY(hipGetLastError());
     return PACKOS_OK;

@@ -69,7 +69,8 @@ struct EncHdr {            // one uint16 header word
     uint16_t j;            // index within the header block
     uint16_t value;        // constant word (h0, or 0x0010 for an empty nested block)
     uint16_t ovf;          // constant word overflowed 13 bits
-    uint16_t pad;
+    uint16_t child;        // container id + 1 of the field this entry starts (0: a leaf / End);
+                           // extended mode: its tag becomes 2 when that container is extended
 };
 
 struct EncCont {
@@ -77,7 +78,21 @@ struct EncCont {
     int16_t valid_col;     // column holding the nil flag, -1 if never nil
     uint16_t hdr_item;
     uint16_t n_kids;
+    uint16_t end_item;     // items of the container's payload: (hdr_item, end_item)
+    uint8_t tag;           // its own tag: Tuple 4 (also the root chain) / Map 7
+    uint8_t pad;
 };
+
+// ADR-001 extended containers (PACKOS_MODE_EXTENDED, include/packos.h): a
+// container whose payload exceeds 8191 bytes (its End offset would be cut to
+// 13 bits by EncodeHeader, typetags/types.go:44-46) is written as
+//   u16 EncodeHeader(0, TypeExtendedTagContainer) = 0x0002 | u16 own tag |
+//   u32 entries e[0..n] (off << 3 | tag, the 16-bit rules widened; e[0] off =
+//   header bytes 4 + 4(n+1), e[n] = End) | payload
+// and the parent entry of such a field carries tag 2.
+constexpr uint32_t kExtMaxPayload = 8191;
+constexpr uint32_t kExtMarker = 0x0002;
+constexpr uint32_t ext_hdr_bytes(uint32_t n_kids) { return 4u + 4u * (n_kids + 1u); }
 
 struct EncProgram {
     const EncItem* items;
@@ -86,6 +101,7 @@ struct EncProgram {
     const uint8_t* lits;
     int32_t n_items, n_hdrs, n_conts, mode;
     int32_t n_lits;
+    int32_t ext;           // PACKOS_MODE_EXTENDED
     const uint32_t* ipk;   // per item: bits 0-15 static size, 16-23 var slot (255 = not var)
     const uint32_t* ihr;   // per item: IT_HDR -> first header entry | count << 16
 };
@@ -185,6 +201,7 @@ struct DecProgram {
     int32_t root;
     int32_t n_nodes, n_kids, n_lits;   // table sizes (for staging into LDS)
     int32_t flat;      // F > 0: the chain is F leaves (no tuple / map), F <= 15: canonical fast path
+    int32_t ext;       // PACKOS_MODE_EXTENDED: tag-2 containers are read (ADR-001)
 };
 
 // Fixed-layout decode fast path.  A blob whose length is B and whose

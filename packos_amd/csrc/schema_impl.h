@@ -57,7 +57,8 @@ struct DeviceTables {
 }  // namespace packos
 
 struct packos_schema {
-    int mode = 0;
+    int mode = 0;                      // PACKOS_MODE_PUTACCESS / PACKOS_MODE_PACKABLE
+    bool ext = false;                  // PACKOS_MODE_EXTENDED (ADR-001 extended containers)
     std::vector<packos::Node> nodes;   // node 0 = K_ROOT (the chain)
     std::vector<int> col_node;         // column -> node
     std::vector<packos_column_info> col_info;
@@ -115,4 +116,10 @@ void read_tune(Tune& t);
 int upload_tables(packos_schema* s, int device, DeviceTables** out);
 // host run of the device decoder over the canonical blob (kernels.hip)
 bool canonical_decodes(const packos_schema* s);
+// extended mode (ADR-001): item sizes of one blob (nil = 0) -> the header
+// items of containers written extended grow to ext_hdr_bytes (bottom-up,
+// children first); returns the bit mask of extended containers
+uint64_t ext_layout_host(const packos_schema* s, std::vector<int64_t>& sz);
+// extended mode: bytes every container's extended header block may add to a blob
+int64_t ext_overhead(const packos_schema* s);
 }  // namespace packos

@@ -17,6 +17,7 @@ ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
 
 MODE_PUTACCESS = 0
 MODE_PACKABLE = 1
+MODE_EXTENDED = 0x100
 
 
 class PackosColumn(C.Structure):
@@ -39,7 +40,7 @@ class OrGet(C.Structure):
 class OrSeq(C.Structure):
     _fields_ = [("buf", C.c_void_p), ("len", C.c_int64), ("count", C.c_int64), ("base", C.c_int64),
                 ("pos", C.c_int64), ("next_off", C.c_int64), ("next_type", C.c_int),
-                ("cur_off", C.c_int64), ("cur_type", C.c_int)]
+                ("cur_off", C.c_int64), ("cur_type", C.c_int), ("xw", C.c_int)]
 
 
 _lib = None
@@ -64,6 +65,9 @@ def lib():
         L.or_encoded_total.restype = C.c_int64
         L.or_decode_batch.argtypes = [C.POINTER(OrSchema), C.c_void_p, C.c_void_p, C.c_uint64,
                                       C.c_size_t, C.POINTER(PackosColumn), C.c_void_p, C.c_int]
+        L.or_decode_batch_mode.argtypes = [C.POINTER(OrSchema), C.c_void_p, C.c_void_p, C.c_uint64,
+                                           C.c_size_t, C.POINTER(PackosColumn), C.c_void_p, C.c_int, C.c_int]
+        L.or_seq_init_ext.argtypes = [C.POINTER(OrSeq), C.c_void_p, C.c_int64, C.c_int]
         L.or_get_init.argtypes = [C.POINTER(OrGet), C.c_void_p, C.c_int64]
         L.or_get_fixed.argtypes = [C.POINTER(OrGet), C.c_int64, C.c_int, C.c_int,
                                    C.POINTER(C.c_int64)]
@@ -215,7 +219,7 @@ class DecodeOut:
 
 
 def decode(chain, arena: np.ndarray, offsets: Optional[np.ndarray], n: int, stride: int = 0,
-           nthreads=1):
+           nthreads=1, mode=0):
     from packos_amd.columns import column_specs
     os_ = OracleSchema(chain)
     out = DecodeOut(column_specs(chain), n)
@@ -224,8 +228,8 @@ def decode(chain, arena: np.ndarray, offsets: Optional[np.ndarray], n: int, stri
     if a.size == 0:
         a = np.zeros(1, np.uint8)
     o = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
-    lib().or_decode_batch(C.byref(os_.s), _ptr(a), _ptr(o), stride, n, out.cols(), _ptr(st),
-                          nthreads)
+    lib().or_decode_batch_mode(C.byref(os_.s), _ptr(a), _ptr(o), stride, n, out.cols(), _ptr(st),
+                               nthreads, mode)
     return out, st[:n]
 
 
