@@ -32,6 +32,7 @@ KIND_NAMES = {1: "int", 2: "uint", 3: "float", 4: "bool", 5: "string", 6: "bytes
 EXPORTED = [
     "packos_schema_compile", "packos_schema_free", "packos_schema_num_columns",
     "packos_schema_num_top_fields", "packos_schema_column_info", "packos_schema_fixed_blob_size",
+    "packos_schema_ext_overhead",
     "packos_schema_decode_fast", "packos_schema_column_default",
     "packos_schema_describe", "packos_schema_blob_size_host", "packos_encode_workspace_size",
     "packos_encoded_size_batch", "packos_encode_batch", "packos_encode_host_batch", "packos_decode_host_batch", "packos_decode_batch",

@@ -86,6 +86,11 @@ class CompiledSchema:
         return int(lib().packos_schema_fixed_blob_size(self._h))
 
     @property
+    def ext_overhead(self) -> int:
+        """MODE_EXTENDED: most bytes extended header blocks add to one blob (0 otherwise)."""
+        return int(lib().packos_schema_ext_overhead(self._h))
+
+    @property
     def decode_fast(self) -> bool:
         """True when decode_batch uses the tiled fixed-layout decoder."""
         return bool(lib().packos_schema_decode_fast(self._h))

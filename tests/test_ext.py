@@ -350,3 +350,30 @@ def test_gpu_ext_roundtrip(seed):
     back = rebuild_columns(chain, o, arena, hc.n)
     a2, o2, _ = gpu_encode(chain, back, EXT)
     assert np.array_equal(o2, offs) and np.array_equal(a2, arena)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("seed", range(10))
+def test_ext_host_sizes_match_oracle(seed, mode):
+    """packos_schema_blob_size_host (shard planning) applies the extended
+    rule exactly like the encoders; packos_schema_ext_overhead bounds it"""
+    from packos_amd.api import CompiledSchema
+    chain = rand_chain(seed + 60)
+    rows = big_rows(chain, 40, seed)
+    hc = HostColumns.from_rows(chain, rows)
+    _, offs, _ = ob.encode(chain, hc, mode | EXT, nthreads=4)
+    s = CompiledSchema(chain, mode | EXT)
+    ncol = len(s.specs)
+    over = s.ext_overhead
+    plain = CompiledSchema(chain, mode)
+    for i in range(hc.n):
+        w = np.zeros(max(ncol, 1), np.uint32)
+        v = np.ones(max(ncol, 1), np.uint8)
+        for c in range(ncol):
+            if hc.offsets[c] is not None:
+                w[c] = int(hc.offsets[c][i + 1]) - int(hc.offsets[c][i])
+            if hc.valid[c] is not None:
+                v[c] = hc.valid[c][i]
+        got = s.blob_size_host(w, v)
+        assert got == int(offs[i + 1] - offs[i]), i
+        assert got <= plain.blob_size_host(w, v) + over
