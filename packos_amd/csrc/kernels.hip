@@ -1779,12 +1779,10 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
         if (V.oseg >= 0) V.seg[V.oseg].src = (const uint8_t*)out_offsets;
         const uint64_t ntiles = (n + kVT - 1) / kVT;
 #ifdef PACKOS_PHASE_PROF
-        static unsigned long long* prof[64] = {};
-        int dev = 0;
-        HIP_TRY(hipGetDevice(&dev));
-        if (!prof[dev]) HIP_TRY(hipMalloc(&prof[dev], 8 * sizeof(unsigned long long)));
-        HIP_TRY(hipMemsetAsync(prof[dev], 0, 8 * sizeof(unsigned long long), st));
-        V.prof = prof[dev];
+        unsigned long long* prof = nullptr;   // debug build only: per-tile phase clocks
+        HIP_TRY(hipMalloc(&prof, ntiles * 8 * sizeof(unsigned long long)));
+        HIP_TRY(hipMemsetAsync(prof, 0, ntiles * 8 * sizeof(unsigned long long), st));
+        V.prof = prof;
 #endif
         // instantiated per var-slot bound: the per-blob loops over var slots
         // (positions, lengths, header offsets) stop at the schema's count
@@ -1806,9 +1804,13 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
 #undef PACKOS_TILES
         HIP_TRY(hipGetLastError());
 #ifdef PACKOS_PHASE_PROF
-        unsigned long long h[8];
-        HIP_TRY(hipMemcpyAsync(h, prof[dev], sizeof(h), hipMemcpyDeviceToHost, st));
+        std::vector<unsigned long long> hp(ntiles * 8);
+        HIP_TRY(hipMemcpyAsync(hp.data(), prof, hp.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipFree(prof));
+        unsigned long long h[8] = {};
+        for (uint64_t x = 0; x < ntiles; x++)
+            for (int q = 0; q < 8; q++) h[q] += hp[x * 8 + q];
         fprintf(stderr, "k_encode_tiles lds=%u tiles=%llu clocks/tile: load=%.0f [round2=%.0f blobs=%.0f scan=%.0f] "
                 "frame=%.0f [chunks1=%.0f chunks2=%.0f]\n",
                 V.lds_total, (unsigned long long)ntiles, (double)h[0] / ntiles, (double)h[4] / ntiles,
