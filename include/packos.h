@@ -378,6 +378,11 @@ int packos_get_field_batch(const uint8_t* arena, const uint64_t* offsets, uint64
 #define PACKOS_GET_SPAN      2
 #define PACKOS_GET_INT       3
 #define PACKOS_GET_FLOAT     4
+/* OR-ed into `getter`: read ADR-001 extended containers (PACKOS_MODE_EXTENDED
+ * blobs): a blob starting 02 00 is an extended top-level chain, a tag-2 field
+ * on the path an extended tuple / map (malformed -> status 1); the final
+ * field's tag is reported as written (2 for an extended container)        */
+#define PACKOS_GET_EXTENDED  0x100
 int packos_get_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride, size_t n_blobs,
                      const int32_t* path, int depth, int getter, int want_tag, int want_width,
                      uint8_t* out_values, uint32_t value_width, uint64_t* out_start, uint32_t* out_len,

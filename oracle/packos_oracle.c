@@ -848,10 +848,31 @@ int or_get_init(or_get* g, const uint8_t* buf, int64_t len) {
     int64_t base = rd16(buf) >> 3;
     if (len < base) return 0;
     g->buf = buf; g->len = len; g->base = base; g->arg_count = base / 2 - 1;
+    g->xw = 0; g->xmode = 0;
+    return 1;
+}
+/* ADR-001 extended container as a GetAccess (this build's format,
+ * include/packos.h): lead 02 00 | kind (4 or 7; top level: 4) | u32 entries */
+static int get_init_ext(or_get* g, const uint8_t* buf, int64_t len, int top) {
+    if (len < 12 || rd16(buf) != or_encode_header(0, PACKOS_TAG_EXTENDED)) return 0;
+    int kind = rd16(buf + 2);
+    if (kind != PACKOS_TAG_TUPLE && (top || kind != PACKOS_TAG_MAP)) return 0;
+    int64_t base = rd32(buf + 4) >> 3;
+    if (base < 12 || (base & 3) || len < base) return 0;
+    g->buf = buf; g->len = len; g->base = base; g->arg_count = (base - 4) / 4 - 1;
+    g->xw = 1; g->xmode = 1;
     return 1;
 }
 void or_get_range(const or_get* g, int64_t pos, int* tp, int64_t* start, int64_t* end) {
     if (pos >= g->arg_count) { *tp = 0; *start = -2; *end = -1; return; }
+    if (g->xw) {
+        uint32_t e1 = rd32(g->buf + 4 + pos * 4), e2 = rd32(g->buf + 4 + (pos + 1) * 4);
+        *start = e1 >> 3; *tp = e1 & 7;
+        *end = (int64_t)(e2 >> 3) + g->base;
+        if (pos > 0) *start += g->base;
+        if (*end > g->len) *end = -1;
+        return;
+    }
     uint16_t h1 = rd16(g->buf + pos * 2), h2 = rd16(g->buf + (pos + 1) * 2);
     *start = h1 >> 3; *tp = h1 & 7;
     *end = (h2 >> 3) + g->base;
@@ -883,10 +904,20 @@ int or_get_span(const or_get* g, int64_t pos, int64_t* start, int64_t* end) {
 int or_get_nested(const or_get* g, int64_t pos, or_get* nested, int* tp) {
     int64_t st, en;
     or_get_range(g, pos, tp, &st, &en);
-    if (en < st || (*tp != 7 && *tp != 4)) return 1;
+    const int x = g->xmode && *tp == PACKOS_TAG_EXTENDED;
+    if (en < st || (*tp != 7 && *tp != 4 && !x)) return 1;
     if (en == st) return 2;
+    if (x) return get_init_ext(nested, g->buf + st, en - st, 0) ? 0 : 1;   /* malformed: decode error */
     if (!or_get_init(nested, g->buf + st, en - st)) return 3; /* nil accessor: later use panics */
+    nested->xmode = g->xmode;
     return 0;
+}
+/* top-level accessor; xmode: a blob starting 02 00 is extended */
+static int get_open(or_get* g, const uint8_t* buf, int64_t len, int xmode) {
+    if (xmode && len >= 2 && rd16(buf) == or_encode_header(0, PACKOS_TAG_EXTENDED)) return get_init_ext(g, buf, len, 1);
+    if (!or_get_init(g, buf, len)) return 0;
+    g->xmode = xmode;
+    return 1;
 }
 
 int or_get_field_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride, size_t n,
@@ -941,13 +972,15 @@ int or_get_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
                  const int32_t* path, int depth, int getter, int want_tag, int want_width,
                  uint8_t* out_values, uint32_t value_width, uint64_t* out_start, uint32_t* out_len,
                  uint8_t* out_tag, uint8_t* status) {
+    const int xmode = (getter & PACKOS_GET_EXTENDED) != 0;
+    getter &= ~PACKOS_GET_EXTENDED;
     for (size_t i = 0; i < n; i++) {
         uint64_t a = offsets ? offsets[i] : i * stride;
         uint64_t b = offsets ? offsets[i + 1] : (i + 1) * stride;
         or_get g;
         out_start[i] = 0; out_len[i] = 0; out_tag[i] = 0;
         if (out_values) memset(out_values + i * value_width, 0, value_width);
-        if (!or_get_init(&g, arena + a, (int64_t)(b - a))) { status[i] = 3; continue; }
+        if (!get_open(&g, arena + a, (int64_t)(b - a), xmode)) { status[i] = 3; continue; }
         uint64_t base = a;
         int st = 0;
         for (int d = 0; d < depth - 1 && !st; d++) {

@@ -129,7 +129,11 @@ int or_seq_next(or_seq* s, int64_t* start, int64_t* width, int* typ);  /* 0 ok *
 int or_seq_peek_nested(const or_seq* s, or_seq* nested);               /* 0 ok */
 
 /* ---- GetAccess restatement (access/get.go) ---- */
-typedef struct or_get { const uint8_t* buf; int64_t len; int64_t arg_count, base; } or_get;
+typedef struct or_get {
+    const uint8_t* buf; int64_t len; int64_t arg_count, base;
+    int xw;      /* 1: an ADR-001 extended container (u32 entries after a 4-byte lead) */
+    int xmode;   /* PACKOS_GET_EXTENDED: tag-2 fields open extended accessors */
+} or_get;
 int  or_get_init(or_get* g, const uint8_t* buf, int64_t len);          /* 0 = nil accessor */
 void or_get_range(const or_get* g, int64_t pos, int* tp, int64_t* start, int64_t* end);
 /* Get{Int,Uint,Float,Bool}XX semantics: tag and exact width; 0 ok, 1 error */

@@ -29,7 +29,7 @@ from .schema import SchemaChain
 __all__ = ["CompiledSchema", "DeviceColumns", "DecodedColumns", "HostDecoded", "encode_batch", "decode_batch",
            "encode_host_batch", "decode_host_batch",
            "get_field_batch", "get_batch", "GET_FIXED", "GET_NULLABLE", "GET_SPAN", "GET_INT",
-           "GET_FLOAT", "MODE_PUTACCESS", "MODE_PACKABLE", "MODE_EXTENDED"]
+           "GET_FLOAT", "GET_EXTENDED", "MODE_PUTACCESS", "MODE_PACKABLE", "MODE_EXTENDED"]
 
 
 def _torch():
@@ -446,6 +446,7 @@ VIEW_DEFAULT = 0x8000000000000000
 
 # getter families of packos_get_batch (include/packos.h)
 GET_FIXED, GET_NULLABLE, GET_SPAN, GET_INT, GET_FLOAT = range(5)
+GET_EXTENDED = 0x100   # OR-ed into a getter: read ADR-001 extended containers (include/packos.h)
 
 
 def get_batch(arena, offsets, n: int, path, getter: int, want_tag: int = 0, want_width: int = 0,
@@ -457,12 +458,14 @@ def get_batch(arena, offsets, n: int, path, getter: int, want_tag: int = 0, want
     GET_NULLABLE (GetNullable*: width 0 -> status 4 before the tag check),
     GET_SPAN (GetBytes/GetString), GET_INT (GetInt: any of 1/2/4/8 bytes,
     sign-extended to int64), GET_FLOAT (GetFloating: 4/8 bytes, raw bits).
+    OR GET_EXTENDED into `getter` to read ADR-001 extended containers.
     `values` is an (n, value_width) uint8 tensor of the gathered typed values
     (None for GET_SPAN or values=False); view it with .view(torch.int64) etc."""
     torch = _torch()
     dev = arena.device
-    vw = 8 if getter in (GET_INT, GET_FLOAT) else max(want_width, 0)
-    gather = values and getter != GET_SPAN and vw > 0
+    fam = getter & ~GET_EXTENDED   # GET_EXTENDED: read MODE_EXTENDED blobs
+    vw = 8 if fam in (GET_INT, GET_FLOAT) else max(want_width, 0)
+    gather = values and fam != GET_SPAN and vw > 0
     vals = torch.empty((max(n, 1), vw), dtype=torch.uint8, device=dev) if gather else None
     s0 = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
     ln = torch.empty(max(n, 1), dtype=torch.int32, device=dev)

@@ -1224,6 +1224,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecPro
 struct DGet {
     uint64_t start;
     int64_t len, base, argc;
+    int xw;   // ADR-001 extended container: u32 entries after a 4-byte lead
 };
 // Byte reader over one blob: its first kGetWin bytes sit in registers (one
 // round of misaligned 16-B loads, whole loads inside the blob only), the rest
@@ -1246,19 +1247,32 @@ struct GWin {
         return a[p];
     }
     __device__ __forceinline__ uint32_t u16(uint64_t p) const { return byte(p) | (byte(p + 1) << 8); }
+    __device__ __forceinline__ uint32_t u32(uint64_t p) const { return u16(p) | (u16(p + 2) << 16); }
 };
 __device__ __forceinline__ bool dget_init(DGet& g, const GWin& r, uint64_t start, int64_t len) {
     if (len < 2) return false;
     g.base = r.u16(start) >> 3;
     if (len < g.base) return false;
-    g.start = start; g.len = len; g.argc = g.base / 2 - 1;
+    g.start = start; g.len = len; g.argc = g.base / 2 - 1; g.xw = 0;
+    return true;
+}
+// extended container (PACKOS_GET_EXTENDED): lead 02 00 | kind (top: 4; nested:
+// 4 or 7) | u32 entries
+__device__ __forceinline__ bool dget_init_ext(DGet& g, const GWin& r, uint64_t start, int64_t len, bool top) {
+    if (len < 12 || r.u16(start) != kExtMarker) return false;
+    const uint32_t kind = r.u16(start + 2);
+    if (kind != PACKOS_TAG_TUPLE && (top || kind != PACKOS_TAG_MAP)) return false;
+    g.base = r.u32(start + 4) >> 3;
+    if (g.base < 12 || (g.base & 3) || len < g.base) return false;
+    g.start = start; g.len = len; g.argc = (g.base - 4) / 4 - 1; g.xw = 1;
     return true;
 }
 // rangeAt (get.go:38-58)
 __device__ __forceinline__ void dget_range(const DGet& g, const GWin& r, int64_t pos, int& tp, int64_t& s,
                                            int64_t& e) {
     if (pos >= g.argc) { tp = 0; s = -2; e = -1; return; }
-    const uint32_t h1 = r.u16(g.start + pos * 2), h2 = r.u16(g.start + (pos + 1) * 2);
+    const uint32_t h1 = g.xw ? r.u32(g.start + 4 + pos * 4) : r.u16(g.start + pos * 2);
+    const uint32_t h2 = g.xw ? r.u32(g.start + 4 + (pos + 1) * 4) : r.u16(g.start + (pos + 1) * 2);
     s = h1 >> 3; tp = h1 & 7;
     e = (h2 >> 3) + g.base;
     if (pos > 0) s += g.base;
@@ -1297,15 +1311,27 @@ __global__ __launch_bounds__(kBlock) void k_get_field(const uint8_t* __restrict_
     uint8_t* dst = out_values ? out_values + i * value_width : nullptr;
     if (dst)
         for (uint32_t k = 0; k < value_width; k++) dst[k] = 0;
+    const bool xmode = (getter & PACKOS_GET_EXTENDED) != 0;
+    getter &= ~PACKOS_GET_EXTENDED;
     DGet g;
-    if (!dget_init(g, r, a0, (int64_t)(a1 - a0))) { status[i] = 3; return; }
+    const bool xtop = xmode && a1 - a0 >= 2 && r.u16(a0) == kExtMarker;
+    if (!(xtop ? dget_init_ext(g, r, a0, (int64_t)(a1 - a0), true) : dget_init(g, r, a0, (int64_t)(a1 - a0)))) {
+        status[i] = 3;
+        return;
+    }
     int tp; int64_t s, e;
     for (int d = 0; d < depth - 1; d++) {
         dget_range(g, r, path.p[d], tp, s, e);
-        if (e < s || (tp != 7 && tp != 4)) { status[i] = 1; return; }
+        const bool x = xmode && tp == PACKOS_TAG_EXTENDED;
+        if (e < s || (tp != 7 && tp != 4 && !x)) { status[i] = 1; return; }
         if (e == s) { status[i] = 2; return; }
         DGet nx;
-        if (!dget_init(nx, r, g.start + (uint64_t)s, e - s)) { status[i] = 3; return; }
+        if (x) {
+            if (!dget_init_ext(nx, r, g.start + (uint64_t)s, e - s, false)) { status[i] = 1; return; }
+        } else if (!dget_init(nx, r, g.start + (uint64_t)s, e - s)) {
+            status[i] = 3;
+            return;
+        }
         g = nx;
     }
     dget_range(g, r, path.p[depth - 1], tp, s, e);
@@ -1924,7 +1950,8 @@ int packos_get_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t str
                      uint64_t* out_start, uint32_t* out_len, uint8_t* out_tag, uint8_t* status, void* stream) {
     if (!path || depth < 1 || depth > 16 || !out_start || !out_len || !out_tag || !status || (!arena && n))
         return PACKOS_E_INVALID;
-    if (getter < PACKOS_GET_FIXED || getter > PACKOS_GET_FLOAT) {
+    const int g_base = getter & ~PACKOS_GET_EXTENDED;
+    if (g_base < PACKOS_GET_FIXED || g_base > PACKOS_GET_FLOAT) {
         set_error("unknown getter");
         return PACKOS_E_INVALID;
     }

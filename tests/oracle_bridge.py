@@ -34,7 +34,7 @@ class OrSchema(C.Structure):
 
 class OrGet(C.Structure):
     _fields_ = [("buf", C.c_void_p), ("len", C.c_int64), ("arg_count", C.c_int64),
-                ("base", C.c_int64)]
+                ("base", C.c_int64), ("xw", C.c_int), ("xmode", C.c_int)]
 
 
 class OrSeq(C.Structure):
@@ -256,8 +256,9 @@ def get_batch(arena, offsets, n, path, getter, want_tag=0, want_width=0, stride=
         a = np.zeros(1, np.uint8)
     o = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
     p = np.asarray(path, dtype=np.int32)
-    vw = 8 if getter in (3, 4) else max(want_width, 0)
-    gather = values and getter != 2 and vw > 0
+    fam = getter & 0xFF
+    vw = 8 if fam in (3, 4) else max(want_width, 0)
+    gather = values and fam != 2 and vw > 0
     vals = np.zeros((max(n, 1), vw), np.uint8) if gather else None
     s0 = np.zeros(max(n, 1), np.uint64)
     ln = np.zeros(max(n, 1), np.uint32)

@@ -377,3 +377,59 @@ def test_ext_host_sizes_match_oracle(seed, mode):
         got = s.blob_size_host(w, v)
         assert got == int(offs[i + 1] - offs[i]), i
         assert got <= plain.blob_size_host(w, v) + over
+
+
+GETTERS = [(0, 1, 2), (0, 1, 8), (1, 1, 4), (1, 3, 8), (2, 6, 0), (3, 0, 0), (4, 0, 0), (0, 5, 1)]
+
+
+def test_ext_oracle_get_reads_extended():
+    """GetAccess over an extended blob (PACKOS_GET_EXTENDED): the nested
+    extended tuple's fields are reached through its tag-2 entry"""
+    chain = SChain(SInt16, STuple(SVariableString(), SInt32), STuple(SBool))
+    s = "x" * 9000
+    arena, offs, _ = enc(chain, [[7, [s, 0x01020304], [True]]], EXT)
+    X = 0x100
+    v, st0, ln, tg, stt = ob.get_batch(arena, offs, 1, [1, 1], 0 | X, 1, 4)
+    assert stt[0] == 0 and int.from_bytes(bytes(v[0]), "little") == 0x01020304
+    v, st0, ln, tg, stt = ob.get_batch(arena, offs, 1, [1, 0], 2 | X, 6, 0)
+    assert stt[0] == 0 and ln[0] == 9000 and bytes(arena[st0[0]:st0[0] + 9000]) == s.encode()
+    v, st0, ln, tg, stt = ob.get_batch(arena, offs, 1, [0], 3 | X)
+    assert stt[0] == 0 and int.from_bytes(bytes(v[0]), "little") == 7
+    assert ob.get_batch(arena, offs, 1, [1], 2 | X, 6, 0)[3][0] == 2      # the field's own tag: 2
+    # without the flag the reference's GetAccess sees h0 offset 0 (argCount
+    # -1): every Get* is a decode error
+    assert ob.get_batch(arena, offs, 1, [0], 3)[4][0] == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(12))
+def test_gpu_ext_get_batch(seed):
+    """packos_get_batch | PACKOS_GET_EXTENDED vs the oracle on extended
+    batches (every getter family, random nested paths, some corrupted blobs)"""
+    from packos_amd.api import get_batch
+    T = _torch()
+    rng = np.random.default_rng(500 + seed)
+    chain = rand_chain(seed)
+    rows = big_rows(chain, 150, seed)
+    arena, offs, _ = enc(chain, rows, int(rng.integers(0, 2)) | EXT)
+    arena = arena.copy()
+    for i in range(0, len(rows), 4):
+        a, b = int(offs[i]), int(offs[i + 1])
+        if b > a:
+            arena[a + int(rng.integers(0, min(12, b - a)))] = rng.integers(0, 256)
+    da = T.from_numpy(arena).to("cuda:0")
+    do = T.from_numpy(offs.astype(np.int64)).to("cuda:0")
+    for _ in range(12):
+        depth = int(rng.integers(1, 3))
+        path = [int(rng.integers(0, 6)) for _ in range(depth)]
+        getter, tag, width = GETTERS[int(rng.integers(0, len(GETTERS)))]
+        o = ob.get_batch(arena, offs, len(rows), path, getter | 0x100, tag, width)
+        g = [None if x is None else x.cpu().numpy()
+             for x in get_batch(da, do, len(rows), path, getter | 0x100, tag, width)]
+        what = (path, getter, tag, width)
+        assert np.array_equal(o[4], g[4]), what
+        assert np.array_equal(o[3], g[3]), what
+        assert np.array_equal(o[1], g[1].astype(np.uint64)), what
+        assert np.array_equal(o[2], g[2].astype(np.uint32)), what
+        if o[0] is not None:
+            assert np.array_equal(o[0], g[0]), what
