@@ -919,11 +919,14 @@ int packos_schema_compile(const char* schema_json, int mode, packos_schema** out
         b.build_encode();
         {   // static prefix read by the decoder's per-blob window
             int64_t pre = 0;
+            bool var = false, tail = false;
             for (const EncItem& it : s->items) {
-                if (it.type == IT_VAR) break;
-                pre += it.size;
+                if (it.type == IT_VAR) var = true;
+                else if (var) tail = true;
+                if (!var) pre += it.size;
             }
             s->dec_prefix = pre;
+            s->dec_tail_fixed = tail;
         }
         b.build_fixed();
         b.build_decode();

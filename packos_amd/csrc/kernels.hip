@@ -1009,7 +1009,9 @@ __global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols col
         // dword k of thread t's window at win32[k * kBlock + t]
         w = win + 4 * tid;
         b0 = a0 & ~15ull;
-        const uint64_t end = min(a1, b0 + 16ull * WC);
+        // only the bytes the decoder reads: the static prefix when nothing but
+        // var payloads (returned as views) follows it
+        const uint64_t end = min(a1, P.win > 0 ? min(a0 + (uint64_t)P.win, b0 + 16ull * WC) : b0 + 16ull * WC);
         const uint32_t nch = (i < n && end > a0) ? (uint32_t)((end - b0 + 15) >> 4) : 0u;
         u32x4 v[WC];
 #pragma unroll
@@ -1029,7 +1031,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols col
     __syncthreads();
     if (i >= n) return;
     const WReader R{arena, (const uint32_t*)w, b0, wbytes, tile_mode ? 1u : (uint32_t)kBlock};
-    const DecProgram LP{lnodes, lkids, llits, P.root, P.n_nodes, P.n_kids, P.n_lits, P.flat, P.ext};
+    const DecProgram LP{lnodes, lkids, llits, P.root, P.n_nodes, P.n_kids, P.n_lits, P.flat, P.ext, P.win};
     uint32_t sv = kFlatFallback;
     if (P.flat) sv = decode_flat(LP, cols, R, a0, a1, i);
     if (sv == kFlatFallback) sv = decode_blob<WReader, EXT>(LP, cols, R, a0, a1, i);
@@ -1524,6 +1526,7 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     t.dec.n_kids = (int32_t)s->dkids.size();
     t.dec.n_lits = (int32_t)s->lits.size();
     t.dec.ext = s->ext ? 1 : 0;
+    t.dec.win = s->has_var && !s->dec_tail_fixed && !s->ext ? (int32_t)s->dec_prefix : 0;
     {   // flat chain of <= 15 leaves: the canonical fast path applies
         const Node& root = s->nodes[0];
         bool flat = !root.kids.empty() && root.kids.size() <= 15;

@@ -202,6 +202,8 @@ struct DecProgram {
     int32_t n_nodes, n_kids, n_lits;   // table sizes (for staging into LDS)
     int32_t flat;      // F > 0: the chain is F leaves (no tuple / map), F <= 15: canonical fast path
     int32_t ext;       // PACKOS_MODE_EXTENDED: tag-2 containers are read (ADR-001)
+    int32_t win;       // > 0: the decoder reads nothing past this many leading blob bytes but
+                       // var views (no fixed field / header after the first var payload)
 };
 
 // Fixed-layout decode fast path.  A blob whose length is B and whose

@@ -100,6 +100,7 @@ struct packos_schema {
     std::vector<uint8_t> canon;       // all-present blob, zero payload bytes
     int dec_fast = 0;                 // 1: canonical blob decodes (set at compile)
     int64_t dec_prefix = 0;           // bytes of an all-present blob before its first var payload
+    bool dec_tail_fixed = false;      // some header / fixed / literal item follows the first var item
 
     packos::Tune tune;
 
