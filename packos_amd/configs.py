@@ -141,6 +141,20 @@ def c5_lengths(n: int, seed: int, lo: int = 0) -> Dict[int, np.ndarray]:
     return {3: ls.astype(np.uint32), 4: lb.astype(np.uint32)}
 
 
+def x1_lengths(n: int, seed: int, lo: int = 0) -> Dict[int, np.ndarray]:
+    """Blob size log-uniform in [2 KiB, 64 KiB] (B = 12 (H) + 8 + ls + lb):
+    about three quarters of the blobs pass 8191 bytes."""
+    r = splitmix64(seed ^ 0x1111, n, start=lo).astype(np.float64) / 2.0 ** 64
+    B = np.floor(np.exp(np.log(2048.0) + r * (np.log(65536.0) - np.log(2048.0)))).astype(np.int64)
+    rest = np.clip(B, 2048, 65536) - 20
+    ls = rest // 3
+    return {1: ls.astype(np.uint32), 2: (rest - ls).astype(np.uint32)}
+
+
+# X1 (beyond BASELINE.json): ADR-001 extended containers, PACKOS_MODE_EXTENDED
+CHAIN_X1 = SChain(SInt64, SVariableString(), SVariableBytes())
+MODE_EXTENDED = 0x100
+
 CONFIGS = {
     "M": Config("M", CHAIN_M, 1 << 20, 0x5EED0001,
                 note="1M x 256 B fixed-schema tuples (metric)"),
@@ -151,6 +165,8 @@ CONFIGS = {
     "C4": Config("C4", CHAIN_C4, 4 << 20, 0x5EED0004, note="4M x 256 B with nested PackMapSorted"),
     "C5": Config("C5", CHAIN_C5, 64 << 20, 0x5EED0005, var_len=c5_lengths, per_gpu=(64 << 20) // 8,
                  note="64M mixed 64 B-4 KB across 8 GPUs (one GPU = one 8,388,608-blob shard)"),
+    "X1": Config("X1", CHAIN_X1, 1 << 16, 0x5EED00E1, mode=MODE_EXTENDED, var_len=x1_lengths,
+                 note="64k blobs of 2-64 KiB, extended containers (ADR-001, beyond BASELINE)"),
 }
 
 

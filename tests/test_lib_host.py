@@ -56,7 +56,7 @@ def test_config_blob_sizes():
 
 def test_decode_fast_eligibility_configs():
     fast = {k: CompiledSchema(c.chain, c.mode).decode_fast for k, c in CONFIGS.items()}
-    assert fast == {"M": True, "C1": True, "C2": True, "C3": False, "C4": True, "C5": False}
+    assert fast == {"M": True, "C1": True, "C2": True, "C3": False, "C4": True, "C5": False, "X1": False}
     from packos_amd.schema import SChain, STuple, SInt32
     # a present empty tuple is written as 10 00, which DecodeBuffer rejects
     assert not CompiledSchema(SChain(SInt32, STuple())).decode_fast
