@@ -1805,7 +1805,10 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
             if ((r = size_pass(s, t, ec, n, out_offsets, ws, ws_bytes, st))) return r;
         }
         V.lits = t->enc.lits;
-        if (V.oseg >= 0) V.seg[V.oseg].src = (const uint8_t*)out_offsets;
+        if (V.oseg >= 0) {
+            V.seg[V.oseg].src = (const uint8_t*)out_offsets;
+            V.seg[V.oseg].r0 = V.seg[V.oseg].lds + (uint32_t)((uintptr_t)out_offsets & 15);
+        }
         const uint64_t ntiles = (n + kVT - 1) / kVT;
 #ifdef PACKOS_PHASE_PROF
         unsigned long long* prof = nullptr;   // debug build only: per-tile phase clocks
