@@ -238,9 +238,11 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_tile(FixProgram P, FixS
     for (int g = 0; g < S.n; g++) {
         const uint32_t nch = (T * S.c[g].width) >> 4;
         const uint8_t* cbase = S.c[g].base + blob0 * S.c[g].width;
+        // in a register: dma16's memory clobber would make the compiler re-read
+        // the kernel argument (a scalar load + wait) before every DMA
+        const uint32_t lbase = lds0 + S.c[g].lds_off;
         for (uint32_t c0 = wv * kWave; c0 < nch; c0 += kBlock) {
-            if (c0 + lane < nch)
-                dma16(cbase + (c0 + lane) * 16u, __builtin_amdgcn_readfirstlane(lds0 + S.c[g].lds_off + c0 * 16u));
+            if (c0 + lane < nch) dma16(cbase + (c0 + lane) * 16u, __builtin_amdgcn_readfirstlane(lbase + c0 * 16u));
         }
     }
     // descriptors (their global loads queue behind the DMA)
