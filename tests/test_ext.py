@@ -433,3 +433,26 @@ def test_gpu_ext_get_batch(seed):
         assert np.array_equal(o[2], g[2].astype(np.uint32)), what
         if o[0] is not None:
             assert np.array_equal(o[0], g[0]), what
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(4))
+def test_gpu_ext_decode_host_batch(seed):
+    """packos_decode_host_batch in extended mode (host arena -> chunked H2D ->
+    decode -> host columns) vs the oracle"""
+    from packos_amd.api import CompiledSchema, decode_host_batch
+    chain = rand_chain(seed + 80)
+    rows = big_rows(chain, 200, seed)
+    arena, offs, _ = enc(chain, rows, EXT)
+    n = len(rows)
+    got, g_st = decode_host_batch(CompiledSchema(chain, EXT), arena, offs, n, chunk_blobs=37)
+    o_out, o_st = ob.decode(chain, arena, offs, n, nthreads=8, mode=EXT)
+    assert np.array_equal(o_st, g_st)
+    ok = o_st[:n] == 0
+    for c, sp in enumerate(o_out.specs):
+        if sp.fixed:
+            w = sp.width
+            assert np.array_equal(o_out.data[c][: n * w].reshape(n, w)[ok], got.data[c][: n * w].reshape(n, w)[ok])
+        if sp.var:
+            assert np.array_equal(o_out.start[c][:n][ok], got.start[c][:n][ok])
+            assert np.array_equal(o_out.length[c][:n][ok], got.length[c][:n][ok])
