@@ -55,8 +55,64 @@ def parse():
     p.add_argument("--op", default="encode", choices=["encode", "decode", "get"],
                    help="decode: schema.DecodeBuffer over the encoded shard; get: GetAccess GetInt of "
                         "top-level field --get-pos with the typed gather (per-config tables, not the metric)")
-    p.add_argument("--get-pos", type=int, default=2)
+    p.add_argument("--get-pos", type=int, default=-1,
+                   help="top-level field GetInt reads (default: the config's first int64 field)")
     return p.parse_args()
+
+
+# ----------------------------------------------------------------- bytes
+LINE = 128   # L2 cache line (bytes): the smallest unit a scattered read fetches
+
+
+def lines_touched(a0, end, line=LINE):
+    """Distinct `line`-byte lines covered by the ordered, disjoint byte windows
+    [a0[i], end[i]) (empty windows skipped)."""
+    a0 = np.asarray(a0, dtype=np.uint64)
+    end = np.asarray(end, dtype=np.uint64)
+    m = end > a0
+    a0, end = a0[m], end[m]
+    if a0.size == 0:
+        return 0
+    first = a0 // np.uint64(line)
+    last = (end - np.uint64(1)) // np.uint64(line)
+    return int((last - first + np.uint64(1)).sum()) - int(np.count_nonzero(first[1:] == last[:-1]))
+
+
+def top_layout(chain):
+    """(header bytes, [(kind, width) per top-level field]) of a flat chain;
+    width 0 = variable."""
+    fields = []
+    for node in chain.Schemas:
+        if node.kind in ("int", "uint", "float", "bool") or (node.kind in ("string", "bytes", "match")):
+            fields.append((node.kind, node.width if node.width and node.width > 0 else 0))
+        else:
+            fields.append((node.kind, -1))   # container
+    return 2 * (len(fields) + 1), fields
+
+
+def static_prefix(chain):
+    """Bytes of a flat blob before its first variable payload (header block +
+    the fixed fields in front), and whether any fixed payload follows a var
+    one; None for chains with containers."""
+    H, fields = top_layout(chain)
+    if any(w < 0 for _, w in fields):
+        return None, True
+    pre, seen_var, tail_fixed = H, False, False
+    for _, w in fields:
+        if w == 0:
+            seen_var = True
+        elif seen_var:
+            tail_fixed = True
+        else:
+            pre += w
+    return pre, tail_fixed
+
+
+def first_int64(chain):
+    for j, node in enumerate(chain.Schemas):
+        if node.kind == "int" and node.width == 8:
+            return j
+    return 0
 
 
 # ----------------------------------------------------------------- host info
@@ -96,8 +152,12 @@ def cpu_leg(cfg, hc, seconds, gpu_arena, gpu_offsets):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bridge as ob  # checker / baseline only
     hi = host_info()
-    threads = max(1, min(1024, hi["affinity"] or hi["nproc"]))
-    threads = max(1, min(threads, hc.n // 4096))   # >= 4096 blobs per thread (C1's 1k blobs: one)
+    aff = max(1, min(1024, hi["affinity"] or hi["nproc"]))
+    quota = hi["cgroup_cpu_quota"]
+    eff = max(1, min(aff, int(quota))) if quota else aff   # CPUs this process can actually keep busy
+    hi["effective_cpus"] = eff
+    cap = max(1, hc.n // 4096)   # >= 4096 blobs per thread (C1's 1k blobs: one)
+    cands = sorted({min(eff, cap), min(aff, cap)})
     os_ = ob.OracleSchema(cfg.chain)
     keep = []
     cols = ob.make_cols(hc, keep)
@@ -106,9 +166,10 @@ def cpu_leg(cfg, hc, seconds, gpu_arena, gpu_offsets):
     arena = np.empty(max(total, 1), np.uint8)
     offs = np.empty(n + 1, np.uint64)
     res = {}
-    for label, th in (("mt", threads), ("st", 1)):
+    legs = [(f"mt{th}", th) for th in cands] + [("st", 1)]
+    for label, th in legs:
         passes, t0 = 0, time.perf_counter()
-        budget = seconds if label == "mt" else seconds / 2
+        budget = seconds / len(cands) if label != "st" else seconds / 2
         while True:
             r = ob.lib().or_encode_batch(ob.C.byref(os_.s), cols, n, cfg.mode, arena.ctypes.data, arena.size,
                                          offs.ctypes.data, None, th)
@@ -118,11 +179,32 @@ def cpu_leg(cfg, hc, seconds, gpu_arena, gpu_offsets):
             if el >= budget:
                 break
         res[label] = (passes * n / el, passes, el, th)
+    res["mt"] = max((v for k, v in res.items() if k.startswith("mt")), key=lambda v: v[0])
+    res["tried"] = {v[3]: round(v[0] / 1e6, 3) for k, v in res.items() if k.startswith("mt")}
     same = bool(np.array_equal(arena[:total], gpu_arena[:total]))
     if gpu_offsets is not None:
         same = same and bool(np.array_equal(offs, gpu_offsets.astype(np.uint64)))
     digest = hashlib.sha256(gpu_arena[:total].tobytes()).hexdigest()[:16]
     return res, hi, same, digest, total
+
+
+def shard_parity(cfg, hc, gpu_arena, gpu_offsets, threads):
+    """One oracle encode of this rank's slice, compared with its GPU output."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bridge as ob  # checker only
+    os_ = ob.OracleSchema(cfg.chain)
+    keep = []
+    cols = ob.make_cols(hc, keep)
+    n = hc.n
+    total = int(gpu_offsets[n]) if gpu_offsets is not None else len(gpu_arena)
+    arena = np.empty(max(total, 1), np.uint8)
+    offs = np.empty(n + 1, np.uint64)
+    r = ob.lib().or_encode_batch(ob.C.byref(os_.s), cols, n, cfg.mode, arena.ctypes.data, arena.size,
+                                 offs.ctypes.data, None, threads)
+    same = r == total and bool(np.array_equal(arena[:total], gpu_arena[:total]))
+    if gpu_offsets is not None:
+        same = same and bool(np.array_equal(offs, gpu_offsets.astype(np.uint64)))
+    return same, hashlib.sha256(gpu_arena[:total].tobytes()).hexdigest()[:16]
 
 
 def host_leg(schema, hc):
@@ -255,6 +337,8 @@ def main():
             p.run()
         torch.cuda.synchronize()
         L = _lib.lib()
+        if args.get_pos < 0:
+            args.get_pos = first_int64(cfg.chain)
         path = (C.c_int32 * 1)(args.get_pos)
 
         def get_runner(p):
@@ -301,6 +385,14 @@ def main():
     el, kernel_ms = timed(runs, args.steps, args.warmup)
 
     alg = algorithmic_bytes(hc, total_out, with_offsets=not fixed)
+    gran = None   # granularity-aware bytes: reads counted as whole 128-B lines
+    if args.op != "encode":
+        if fixed:
+            b0 = np.arange(n, dtype=np.uint64) * np.uint64(schema.fixed_blob_size)
+            b1 = b0 + np.uint64(schema.fixed_blob_size)
+        else:
+            o = sets[0].offsets.cpu().numpy().astype(np.uint64)
+            b0, b1 = o[:-1], o[1:]
     if args.op == "decode":
         # DecodeBuffer reads every blob byte except var payloads (returned as
         # views, never read) + the offsets; writes columns, views, validity, status
@@ -310,11 +402,18 @@ def main():
             out_b += n * sp.width if sp.fixed else (12 * n if sp.var else 0)
             out_b += n if sp.has_valid else 0
         alg = total_out - var_bytes + (0 if fixed else 8 * (n + 1)) + out_b
+        pre, tail_fixed = static_prefix(cfg.chain)
+        end = b1 if (pre is None or tail_fixed) else np.minimum(b1, b0 + np.uint64(pre))
+        gran = LINE * lines_touched(b0, end) + (0 if fixed else 8 * (n + 1)) + out_b
     elif args.op == "get":
         # GetAccess rangeAt: h0 + the two header words around the field + its
         # payload (8 B for an int64) in; value 8 + start 8 + len 4 + tag 1 +
         # status 1 out; + the blob offsets for var layouts
         alg = n * (2 + 4 + 8) + n * 22 + (0 if fixed else 8 * (n + 1))
+        H, flds = top_layout(cfg.chain)
+        pay_end = H + sum(w for _, w in flds[:args.get_pos + 1])
+        end = np.minimum(b1, b0 + np.uint64(max(pay_end, 2 * args.get_pos + 4)))
+        gran = LINE * lines_touched(b0, end) + n * 22 + (0 if fixed else 8 * (n + 1))
     blobs = n_global * args.steps
     value = blobs / el / 1e6
     achieved = alg / (kernel_ms * 1e-3) / 1e9
@@ -325,15 +424,19 @@ def main():
     # its provenance, is read from profiles/ when present.
     traffic, traffic_src = None, None
     pmc_name = f"pmc_{args.config}.json" if args.op == "encode" else f"pmc_{args.config}_{args.op}.json"
-    pmc_path = os.path.join(ROOT, "profiles", "r02", pmc_name)
-    if os.path.exists(pmc_path):
+    for rnd in ("r03", "r02"):
+        pmc_path = os.path.join(ROOT, "profiles", rnd, pmc_name)
+        if not os.path.exists(pmc_path):
+            continue
         try:
             with open(pmc_path) as f:
                 pmc = json.load(f)
             traffic = pmc.get("hbm_bytes_per_launch")
-            traffic_src = f"profiles/r02/{pmc_name}: {pmc.get('source', '')}"
+            traffic_src = (f"profiles/{rnd}/{pmc_name}, measured at commit {pmc.get('commit', 'unstamped')}: "
+                           f"{pmc.get('source', '')}")
         except Exception:
             traffic = None
+        break
 
     cpu, parity, host = None, None, None
     if args.op != "encode":
@@ -343,15 +446,31 @@ def main():
         gpu_offs = None if fixed else sets[0].offsets.cpu().numpy()
         res, hi_, same, digest, tot = cpu_leg(cfg, hc, args.cpu_seconds, gpu_arena, gpu_offs)
         mt = res["mt"]
-        cpu = {"value": round(mt[0] / 1e6, 4), "unit": "million blobs/s", "cores": mt[3], "kind": "port",
+        cpu = {"value": round(mt[0] / 1e6, 4), "unit": "million blobs/s", "cores": hi_["effective_cpus"],
+               "kind": "port",
                "sample": f"the whole shard ({n} blobs of config {args.config}), {mt[1]} passes in {mt[2]:.1f} s; "
-                         f"C restatement of PutAccess/Pack (oracle/), {mt[3]} threads = every CPU this "
-                         f"process may run on",
+                         f"C restatement of PutAccess/Pack (oracle/) on {mt[3]} threads, the faster of "
+                         f"{sorted(res['tried'])} threads (cgroup-quota CPUs and affinity CPUs)",
+               "threads": mt[3], "threads_tried_mblobs_s": res["tried"],
                "single_thread_value": round(res['st'][0] / 1e6, 4),
                "nproc": hi_["nproc"], "affinity": hi_["affinity"], "cgroup_cpu_quota": hi_["cgroup_cpu_quota"],
                "cpu_model": hi_["cpu_model"]}
         parity = {"result": "bit-exact" if same else "MISMATCH", "blobs": n, "bytes": tot,
                   "sha256_16": digest, "checked": "GPU arena of the timed run vs the CPU oracle, whole shard"}
+    if world > 1 and not args.no_cpu and args.op == "encode":
+        # every rank checks its own shard against the CPU oracle's encoding of
+        # the same slice (SCALE runs carry correctness); flags meet in a MIN
+        gpu_arena = sets[0].out[:total_out].cpu().numpy()
+        gpu_offs = None if fixed else sets[0].offsets.cpu().numpy()
+        hi_ = host_info()
+        th = max(1, (int(hi_["cgroup_cpu_quota"] or 0) or hi_["affinity"] or 1) // max(1, int(
+            os.environ.get("LOCAL_WORLD_SIZE", world))))
+        same, digest = shard_parity(cfg, hc, gpu_arena, gpu_offs, th)
+        flag = torch.tensor([1 if same else 0], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        parity = {"result": "bit-exact" if int(flag.item()) == 1 else "MISMATCH", "ranks": world,
+                  "blobs_rank0": n, "sha256_16_rank0": digest,
+                  "checked": "every rank: its GPU shard vs the CPU oracle's encoding of the same global slice"}
     if rank == 0 and world == 1 and not args.no_host:
         try:
             host = host_leg(schema, make_columns(cfg, n=min(n, 1 << 22), lo=lo))
@@ -383,6 +502,10 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": alg,
+                         **({} if gran is None else {
+                             "granularity_bytes_per_launch": gran,
+                             "frac_granularity": round(gran / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             "granularity_rule": f"reads counted as whole {LINE}-B lines (union over blobs)"}),
                          "cache_state": f"cold: {len(sets)} sets rotated ({footprint / 2 ** 20:.0f} MiB > 256 MiB "
                                         "Infinity Cache)"},
             "warm": None if warm_kms is None else {

@@ -16,6 +16,8 @@
  *   packos_decode_batch    <- schema.DecodeBuffer / DecodeBufferNamed / ValidateBuffer
  *                             over access.SeqGetAccess                  schema/schema.go:880,893,948; access/seqget.go
  *   packos_get_field_batch <- access.GetAccess Get*(pos) / GetNestedGetAccess  access/get.go:19-375,492
+ *   packos_get_batch          + GetInt / GetFloating / GetTypeAndValue      access/get.go:120-170,504-536
+ *   packos_get_map_batch   <- GetMapStr / GetMapAny / GetMapOrderedAny       access/get.go:412-490
  *   packos_strerror        <- Go error strings (errors.New / SchemaError.Error)
  *
  * Conventions
@@ -113,7 +115,7 @@ extern "C" {
  * bits 24..29 encode only: the ErrorCode of the leaf error that EncodeValue
  *             wraps in ErrEncode (schema.go:919-936), e.g. ErrOutOfRange for
  *             a Range violation; bits 0..7 then hold PACKOS_ERR_ENCODE and
- *             bits 8..23 the top-level field that failed first
+ *             bits 8..23 are 0 (position -1, as the wrapping SchemaError)
  * bit 30      the reference would panic (Go runtime index out of range) on
  *             this blob, e.g. a nullable int16 field of width 1
  * bit 31      encode: an offset >= 8192 was truncated to 13 bits exactly as
@@ -230,6 +232,11 @@ int64_t packos_schema_ext_overhead(const packos_schema* s);
  * decodes cleanly), else 0.  Decided at compile time, without a GPU; results
  * never depend on it (non-canonical blobs fall back to the exact decoder).  */
 int  packos_schema_decode_fast(const packos_schema* s);
+/* 1 when the schema has encode-time value checks (int "min"/"max", "date",
+ * string "prefix"/"suffix"): packos_encode_batch / packos_encode_host_batch
+ * then require a status array, since a failing value makes EncodeValue return
+ * ErrEncode (schema/schema.go:919-936), which only the status can report.  */
+int  packos_schema_has_checks(const packos_schema* s);
 /* decodeDefault literal of column `col` (a string leaf): copies at most cap
  * bytes into buf and returns the literal's length (0 = no default, -1 = bad
  * column).                                                                  */
@@ -263,7 +270,8 @@ int packos_encoded_size_batch(const packos_schema* s, const packos_column* cols,
  * itself when no presence depends on the data, else by a size pass first);
  * pass flags PACKOS_ENC_OFFSETS_READY when out_offsets already holds the
  * layout to encode into (e.g. from packos_encoded_size_batch).  For a fixed-size schema out_offsets may be NULL (blob i
- * is at i*B).  status (n, device) may be NULL.  out_capacity is checked only
+ * is at i*B).  status (n, device) may be NULL unless the schema has value
+ * checks (packos_schema_has_checks; PACKOS_E_INVALID then).  out_capacity is checked only
  * when offsets are known on the host side (fixed schemas); for variable
  * schemas blobs that would end past out_capacity are not written and get
  * PACKOS_ERR_ENCODE in their status.  Var-width column offsets must be
@@ -365,19 +373,26 @@ int packos_get_field_batch(const uint8_t* arena, const uint64_t* offsets, uint64
  *                        1/2/4/8 -> int8..int64 (access/get.go:120-146)
  *   PACKOS_GET_FLOAT     GetFloating: tag Floating, width 0 -> nil, 4/8
  *                        (access/get.go:148-170)
+ *   PACKOS_GET_ANY       GetTypeAndValue / GetAsPackable: any tag, end >=
+ *                        start, else status 1 (the reference returns
+ *                        TypeInvalid and a nil value); a position past the
+ *                        field count is status 3 (rangeAt's (-2, -1) slices
+ *                        buf[-2:-1]: a Go panic) (access/get.go:38-45,
+ *                        504-536); out_tag is the header's tag either way
  * Typed gather: when out_values is not NULL, row i of out_values
  * (value_width bytes) receives the value of a successful FIXED / NULLABLE
  * getter (its LE bytes; a Bool as 0/1), or for INT the integer sign-extended
  * to int64, for FLOAT the raw bits (a float32 in the low 4 bytes); zero
  * otherwise.  value_width: want_width for FIXED / NULLABLE, 8 for INT / FLOAT.
  * status: 0 ok, 1 decode error, 2 nil nested accessor (empty container on
- * the path), 3 nil accessor (NewGetAccess would return nil: the reference
- * panics), 4 nil value.                                                      */
+ * the path), 3 the reference panics (NewGetAccess returned nil and is
+ * dereferenced, or GET_ANY past the field count), 4 nil value.              */
 #define PACKOS_GET_FIXED     0
 #define PACKOS_GET_NULLABLE  1
 #define PACKOS_GET_SPAN      2
 #define PACKOS_GET_INT       3
 #define PACKOS_GET_FLOAT     4
+#define PACKOS_GET_ANY       5
 /* OR-ed into `getter`: read ADR-001 extended containers (PACKOS_MODE_EXTENDED
  * blobs): a blob starting 02 00 is an extended top-level chain, a tag-2 field
  * on the path an extended tuple / map (malformed -> status 1); the final
@@ -387,6 +402,36 @@ int packos_get_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t str
                      const int32_t* path, int depth, int getter, int want_tag, int want_width,
                      uint8_t* out_values, uint32_t value_width, uint64_t* out_start, uint32_t* out_len,
                      uint8_t* out_tag, uint8_t* status, void* stream);
+
+/* Map walk over every blob: walk `depth` - 1 positions like packos_get_batch,
+ * then read the map at the last position as the reference's
+ *   PACKOS_MAP_STR  GetMapStr        (access/get.go:464-490): every key and
+ *                   every value must pass GetString (tag String, end >= start)
+ *   PACKOS_MAP_ANY  GetMapAny / GetMapOrderedAny (get.go:412-462): keys pass
+ *                   GetString; values pass GetAny (get.go:377-410): Integer ->
+ *                   GetInt (width 0 = nil, 1/2/4/8), Floating -> GetFloating
+ *                   (0 = nil, 4/8), String -> GetString, Map -> GetMapAny
+ *                   recursively (validated to any depth up to 32 levels),
+ *                   every other tag (End, Tuple, Bool, ...) an error
+ * (OR PACKOS_GET_EXTENDED in to read ADR-001 extended containers).  Pair j of
+ * blob i (in wire order) lands in row i * max_pairs + j of key_start/key_len
+ * (absolute arena offsets of the key bytes) and val_start/val_len/val_tag
+ * (the value's payload span and tag; a nested map value's span is its whole
+ * container, to be read with a longer path); out_pairs[i] = the map's pair
+ * count.  Wire order is what GetMapOrderedAny keeps; building a Go map from
+ * the pairs in order reproduces GetMapStr / GetMapAny (a later duplicate key
+ * overwrites an earlier one).
+ * status: 0 ok, 1 decode error (the call returns an error), 2 nil nested
+ * accessor on the path, 3 nil accessor (the reference dereferences nil:
+ * panic), 4 nil map (empty payload: the call returns nil, nil), 5 ok but
+ * more than max_pairs pairs (the first max_pairs are written), 6 nested maps
+ * deeper than 32 levels (a limit of this implementation).                   */
+#define PACKOS_MAP_STR 0
+#define PACKOS_MAP_ANY 1
+int packos_get_map_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride, size_t n_blobs,
+                         const int32_t* path, int depth, int flags, uint32_t max_pairs, uint32_t* out_pairs,
+                         uint64_t* key_start, uint32_t* key_len, uint64_t* val_start, uint32_t* val_len,
+                         uint8_t* val_tag, uint8_t* status, void* stream);
 
 /* ---- misc ------------------------------------------------------------------ */
 const char* packos_strerror(int code);

@@ -518,7 +518,8 @@ static void* enc_worker(void* arg) {
             for (int tp = 0; j->s->ext && tp < j->s->n_top; tp++) {
                 int inner = enc_check(j->s, j->cols, i, j->s->top_nodes[tp]);
                 if (inner) {
-                    sv |= (uint32_t)PACKOS_ERR_ENCODE | ((uint32_t)(tp + 1) << 8) | ((uint32_t)inner << 24);
+                    /* SchemaError(ErrEncode, ChainName, "", -1, err): position -1 (schema.go:919-936) */
+                    sv |= (uint32_t)PACKOS_ERR_ENCODE | ((uint32_t)inner << 24);
                     break;
                 }
             }
@@ -1016,6 +1017,11 @@ int or_get_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
                 else if (w == 0) r = 4;
                 else if (w != 4 && w != 8) r = 1;
                 break;
+            case PACKOS_GET_ANY:   /* GetTypeAndValue (get.go:504-510) */
+                /* past argCount rangeAt gives (End, -2, -1): end >= start, and
+                 * g.buf[-2:-1] is a Go runtime panic */
+                r = s0 < 0 ? 3 : e0 < s0 ? 1 : 0;
+                break;
             default:
                 r = 1;
         }
@@ -1023,7 +1029,7 @@ int or_get_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
         if (r) continue;
         out_start[i] = base + (uint64_t)s0;
         out_len[i] = (uint32_t)w;
-        if (!out_values || getter == PACKOS_GET_SPAN) continue;
+        if (!out_values || getter == PACKOS_GET_SPAN || getter == PACKOS_GET_ANY) continue;
         const uint8_t* src = g.buf + s0;
         uint8_t* dst = out_values + i * value_width;
         if (getter == PACKOS_GET_INT) {
@@ -1036,6 +1042,128 @@ int or_get_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
         } else {
             for (int64_t k = 0; k < w && k < (int64_t)value_width; k++) dst[k] = src[k];
         }
+    }
+    return 0;
+}
+
+/* GetMapStr / GetMapAny (access/get.go:412-490) over every blob, the
+ * packos_get_map_batch contract (include/packos.h).  The recursion of
+ * GetMapAny -> GetAny -> GetMapAny (get.go:377-430) is restated directly. */
+#define OR_MAP_MAX_DEPTH 32
+/* GetAny (get.go:377-410) of value position pos of map accessor m: 0 ok, 1
+ * error, 3 panic, 6 too deep; a non-empty nested map is walked (depth+1). */
+static int map_walk(const or_get* m, int any, int depth);
+static int get_any_value(const or_get* m, int64_t pos, int any, int depth) {
+    int tp; int64_t st, en;
+    if (!any) {   /* GetString (get.go:359-365) */
+        or_get_range(m, pos, &tp, &st, &en);
+        return (en < st || tp != PACKOS_TAG_STRING) ? 1 : 0;
+    }
+    /* GetAny reads the header at pos (the End header when pos == argCount);
+     * every getter it calls re-reads through rangeAt, which fails there */
+    if (pos >= m->arg_count) return 1;
+    or_get_range(m, pos, &tp, &st, &en);
+    const int64_t w = en - st;
+    switch (tp) {
+        case PACKOS_TAG_INTEGER: return (w == 0 || w == 1 || w == 2 || w == 4 || w == 8) ? 0 : 1;   /* GetInt :120-146 */
+        case PACKOS_TAG_FLOATING: return (w == 0 || w == 4 || w == 8) ? 0 : 1;                      /* GetFloating :148-170 */
+        case PACKOS_TAG_STRING: return en < st ? 1 : 0;                                              /* GetString */
+        case PACKOS_TAG_MAP: case PACKOS_TAG_EXTENDED: {                                            /* GetMapAny :412-436 */
+            const int x = tp == PACKOS_TAG_EXTENDED;
+            if (x && !m->xmode) return 1;
+            if (en < st) return 1;
+            if (en == st) return 0;   /* nil map */
+            or_get nm;
+            if (x) {
+                if (!get_init_ext(&nm, m->buf + st, en - st, 0) || rd16(nm.buf + 2) != PACKOS_TAG_MAP) return 1;
+            } else if (!or_get_init(&nm, m->buf + st, en - st)) {
+                return 3;   /* NewGetAccess nil -> nested.argCount panics */
+            } else {
+                nm.xmode = m->xmode;
+            }
+            if (depth + 1 >= OR_MAP_MAX_DEPTH) return 6;
+            return map_walk(&nm, any, depth + 1);
+        }
+        default: return 1;   /* "GetAny: unsupported type tag" */
+    }
+}
+static int map_walk(const or_get* m, int any, int depth) {
+    for (int64_t j = 0; j < m->arg_count; j += 2) {
+        int tp; int64_t st, en;
+        or_get_range(m, j, &tp, &st, &en);   /* key: GetString */
+        if (en < st || tp != PACKOS_TAG_STRING) return 1;
+        const int r = get_any_value(m, j + 1, any, depth);
+        if (r) return r;
+    }
+    return 0;
+}
+int or_get_map_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride, size_t n,
+                     const int32_t* path, int depth, int flags, uint32_t max_pairs, uint32_t* out_pairs,
+                     uint64_t* key_start, uint32_t* key_len, uint64_t* val_start, uint32_t* val_len,
+                     uint8_t* val_tag, uint8_t* status) {
+    const int xmode = (flags & PACKOS_GET_EXTENDED) != 0;
+    const int any = (flags & ~PACKOS_GET_EXTENDED) == PACKOS_MAP_ANY;
+    for (size_t i = 0; i < n; i++) {
+        uint64_t a = offsets ? offsets[i] : i * stride;
+        uint64_t b = offsets ? offsets[i + 1] : (i + 1) * stride;
+        out_pairs[i] = 0;
+        for (uint32_t j = 0; j < max_pairs; j++) {
+            const size_t k = i * (size_t)max_pairs + j;
+            key_start[k] = 0; key_len[k] = 0; val_start[k] = 0; val_len[k] = 0; val_tag[k] = 0;
+        }
+        or_get g;
+        if (!get_open(&g, arena + a, (int64_t)(b - a), xmode)) { status[i] = 3; continue; }
+        uint64_t base = a;
+        int st = 0;
+        for (int d = 0; d < depth - 1 && !st; d++) {
+            or_get nx; int tp;
+            int r = or_get_nested(&g, path[d], &nx, &tp);
+            if (r) { st = r; break; }
+            base += (uint64_t)(nx.buf - g.buf);
+            g = nx;
+        }
+        if (st) { status[i] = (uint8_t)st; continue; }
+        int tp; int64_t s0, e0;
+        or_get_range(&g, path[depth - 1], &tp, &s0, &e0);
+        const int x = xmode && tp == PACKOS_TAG_EXTENDED;
+        if (e0 < s0 || (tp != PACKOS_TAG_MAP && !x)) { status[i] = 1; continue; }   /* get.go:414-416 */
+        if (e0 == s0) { status[i] = 4; continue; }                                    /* nil map */
+        or_get m;
+        if (x) {
+            if (!get_init_ext(&m, g.buf + s0, e0 - s0, 0) || rd16(m.buf + 2) != PACKOS_TAG_MAP) { status[i] = 1; continue; }
+        } else if (!or_get_init(&m, g.buf + s0, e0 - s0)) {
+            status[i] = 3;
+            continue;
+        } else {
+            m.xmode = xmode;
+        }
+        const uint64_t mb = base + (uint64_t)s0;
+        int r = 0;
+        uint32_t pairs = 0;
+        for (int64_t j = 0; j < m.arg_count && !r; j += 2, pairs++) {
+            int kt; int64_t ks, ke;
+            or_get_range(&m, j, &kt, &ks, &ke);
+            if (ke < ks || kt != PACKOS_TAG_STRING) { r = 1; break; }
+            r = get_any_value(&m, j + 1, any, 0);
+            if (r) break;
+            if (pairs < max_pairs) {
+                int vt; int64_t vs, ve;
+                or_get_range(&m, j + 1, &vt, &vs, &ve);
+                const size_t k = i * (size_t)max_pairs + pairs;
+                key_start[k] = mb + (uint64_t)ks; key_len[k] = (uint32_t)(ke - ks);
+                val_start[k] = mb + (uint64_t)vs; val_len[k] = (uint32_t)(ve - vs); val_tag[k] = (uint8_t)vt;
+            }
+        }
+        if (r) {   /* a failing call returns no map */
+            status[i] = (uint8_t)r;
+            for (uint32_t j = 0; j < max_pairs; j++) {
+                const size_t k = i * (size_t)max_pairs + j;
+                key_start[k] = 0; key_len[k] = 0; val_start[k] = 0; val_len[k] = 0; val_tag[k] = 0;
+            }
+            continue;
+        }
+        out_pairs[i] = pairs;
+        status[i] = pairs > max_pairs ? 5 : 0;
     }
     return 0;
 }

@@ -155,6 +155,10 @@ int or_get_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
                  const int32_t* path, int depth, int getter, int want_tag, int want_width,
                  uint8_t* out_values, uint32_t value_width, uint64_t* out_start, uint32_t* out_len,
                  uint8_t* out_tag, uint8_t* status);
+int or_get_map_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride, size_t n,
+                     const int32_t* path, int depth, int flags, uint32_t max_pairs, uint32_t* out_pairs,
+                     uint64_t* key_start, uint32_t* key_len, uint64_t* val_start, uint32_t* val_len,
+                     uint8_t* val_tag, uint8_t* status);
 
 /* splitmix64 stream (synthetic data generator shared with the Python side) */
 uint64_t or_splitmix64(uint64_t* state);

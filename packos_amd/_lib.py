@@ -12,6 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PACKOS_LIB") or os.path.join(HERE, "libpackos.so")  # override: experiments only
 
+ABI_VERSION = 2        # PACKOS_ABI_VERSION this binding's structs and signatures follow
 MODE_PUTACCESS = 0
 MODE_PACKABLE = 1
 MODE_EXTENDED = 0x100   # ADR-001 extended containers (include/packos.h), OR-ed into a mode
@@ -33,10 +34,10 @@ EXPORTED = [
     "packos_schema_compile", "packos_schema_free", "packos_schema_num_columns",
     "packos_schema_num_top_fields", "packos_schema_column_info", "packos_schema_fixed_blob_size",
     "packos_schema_ext_overhead",
-    "packos_schema_decode_fast", "packos_schema_column_default",
+    "packos_schema_decode_fast", "packos_schema_has_checks", "packos_schema_column_default",
     "packos_schema_describe", "packos_schema_blob_size_host", "packos_encode_workspace_size",
     "packos_encoded_size_batch", "packos_encode_batch", "packos_encode_host_batch", "packos_decode_host_batch", "packos_decode_batch",
-    "packos_get_field_batch", "packos_get_batch", "packos_strerror", "packos_last_error", "packos_abi_version",
+    "packos_get_field_batch", "packos_get_batch", "packos_get_map_batch", "packos_strerror", "packos_last_error", "packos_abi_version",
 ]
 
 
@@ -85,6 +86,8 @@ def lib():
     L.packos_schema_ext_overhead.restype = i64
     L.packos_schema_decode_fast.argtypes = [vp]
     L.packos_schema_decode_fast.restype = C.c_int
+    L.packos_schema_has_checks.argtypes = [vp]
+    L.packos_schema_has_checks.restype = C.c_int
     L.packos_schema_column_default.argtypes = [vp, i32, C.c_char_p, sz]
     L.packos_schema_column_default.restype = i64
     L.packos_schema_describe.argtypes = [vp, C.c_char_p, sz]
@@ -103,10 +106,16 @@ def lib():
                                          vp, vp, vp, vp, vp]
     L.packos_get_batch.argtypes = [vp, vp, u64, sz, C.POINTER(C.c_int32), i32, i32, i32, i32,
                                    vp, u32, vp, vp, vp, vp, vp]
+    L.packos_get_map_batch.argtypes = [vp, vp, u64, sz, C.POINTER(C.c_int32), i32, i32, u32, vp, vp, vp, vp, vp,
+                                       vp, vp, vp]
     L.packos_strerror.argtypes = [i32]
     L.packos_strerror.restype = C.c_char_p
     L.packos_last_error.restype = C.c_char_p
     L.packos_abi_version.restype = i32
+    got = L.packos_abi_version()
+    if got != ABI_VERSION:   # a stale or foreign .so would read packos_column with the wrong stride
+        raise RuntimeError(f"{LIB_PATH}: packos_abi_version() = {got}, this binding needs {ABI_VERSION}; "
+                           "rebuild it with __graft_entry__.build()")
     _lib = L
     return L
 

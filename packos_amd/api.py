@@ -28,8 +28,8 @@ from .schema import SchemaChain
 
 __all__ = ["CompiledSchema", "DeviceColumns", "DecodedColumns", "HostDecoded", "encode_batch", "decode_batch",
            "encode_host_batch", "decode_host_batch",
-           "get_field_batch", "get_batch", "GET_FIXED", "GET_NULLABLE", "GET_SPAN", "GET_INT",
-           "GET_FLOAT", "GET_EXTENDED", "MODE_PUTACCESS", "MODE_PACKABLE", "MODE_EXTENDED"]
+           "get_field_batch", "get_batch", "get_map_batch", "GET_FIXED", "GET_NULLABLE", "GET_SPAN", "GET_INT",
+           "GET_FLOAT", "GET_ANY", "GET_EXTENDED", "MAP_STR", "MAP_ANY", "MODE_PUTACCESS", "MODE_PACKABLE", "MODE_EXTENDED"]
 
 
 def _torch():
@@ -94,6 +94,11 @@ class CompiledSchema:
     def decode_fast(self) -> bool:
         """True when decode_batch uses the tiled fixed-layout decoder."""
         return bool(lib().packos_schema_decode_fast(self._h))
+
+    @property
+    def has_checks(self) -> bool:
+        """True when encode needs a status array (value checks, include/packos.h)."""
+        return bool(lib().packos_schema_has_checks(self._h))
 
     def all_present_size(self) -> int:
         return int(lib().packos_schema_blob_size_host(self._h, None, None))
@@ -196,6 +201,7 @@ def encode_batch(schema: CompiledSchema, cols: DeviceColumns, want_offsets: bool
     dev = cols.data[0].device if cols.data and cols.data[0] is not None else torch.device("cuda")
     st = _stream_ptr(stream)
     arr = cols.ctypes_array()
+    want_status = want_status or schema.has_checks   # checks report through the status only
     status = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if want_status else None
     fixed = (not cols.has_var()) and not cols.any_valid() and schema.fixed_blob_size >= 0
     if fixed:
@@ -259,6 +265,7 @@ def encode_host_batch(schema: CompiledSchema, hc: HostColumns, chunk_blobs: int 
         out = np.empty(host_batch_bound(schema, hc), dtype=np.uint8)
     cap = out.size
     offs = offsets if offsets is not None else np.empty(n + 1, dtype=np.uint64)
+    want_status = want_status or schema.has_checks
     st = status if status is not None else (np.empty(max(n, 1), dtype=np.uint32) if want_status else None)
     check(L.packos_encode_host_batch(schema.handle, arr, n, out.ctypes.data, cap, offs.ctypes.data,
                                      None if st is None else st.ctypes.data, chunk_blobs),
@@ -327,6 +334,7 @@ class EncodePlan:
         self.fixed = (not cols.has_var()) and not cols.any_valid() and schema.fixed_blob_size >= 0
         self._arr = cols.ctypes_array()
         self._stream = stream
+        want_status = want_status or schema.has_checks
         self.status = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if want_status else None
         if self.fixed:
             self.B = schema.all_present_size()
@@ -445,7 +453,8 @@ def get_field_batch(arena, offsets, n: int, path, want_tag: int, want_width: int
 VIEW_DEFAULT = 0x8000000000000000
 
 # getter families of packos_get_batch (include/packos.h)
-GET_FIXED, GET_NULLABLE, GET_SPAN, GET_INT, GET_FLOAT = range(5)
+GET_FIXED, GET_NULLABLE, GET_SPAN, GET_INT, GET_FLOAT, GET_ANY = range(6)
+MAP_STR, MAP_ANY = 0, 1   # packos_get_map_batch: GetMapStr / GetMapAny (include/packos.h)
 GET_EXTENDED = 0x100   # OR-ed into a getter: read ADR-001 extended containers (include/packos.h)
 
 
@@ -457,7 +466,8 @@ def get_batch(arena, offsets, n: int, path, getter: int, want_tag: int = 0, want
     `getter` picks the Get* family: GET_FIXED (Get{Bool,IntN,UintN,FloatN}),
     GET_NULLABLE (GetNullable*: width 0 -> status 4 before the tag check),
     GET_SPAN (GetBytes/GetString), GET_INT (GetInt: any of 1/2/4/8 bytes,
-    sign-extended to int64), GET_FLOAT (GetFloating: 4/8 bytes, raw bits).
+    sign-extended to int64), GET_FLOAT (GetFloating: 4/8 bytes, raw bits),
+    GET_ANY (GetTypeAndValue: any tag, end >= start; span + tag only).
     OR GET_EXTENDED into `getter` to read ADR-001 extended containers.
     `values` is an (n, value_width) uint8 tensor of the gathered typed values
     (None for GET_SPAN or values=False); view it with .view(torch.int64) etc."""
@@ -465,7 +475,7 @@ def get_batch(arena, offsets, n: int, path, getter: int, want_tag: int = 0, want
     dev = arena.device
     fam = getter & ~GET_EXTENDED   # GET_EXTENDED: read MODE_EXTENDED blobs
     vw = 8 if fam in (GET_INT, GET_FLOAT) else max(want_width, 0)
-    gather = values and fam != GET_SPAN and vw > 0
+    gather = values and fam not in (GET_SPAN, GET_ANY) and vw > 0
     vals = torch.empty((max(n, 1), vw), dtype=torch.uint8, device=dev) if gather else None
     s0 = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
     ln = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
@@ -478,3 +488,30 @@ def get_batch(arena, offsets, n: int, path, getter: int, want_tag: int = 0, want
                                  s0.data_ptr(), ln.data_ptr(), tg.data_ptr(), st.data_ptr(), _stream_ptr(stream)),
           "packos_get_batch")
     return (None if vals is None else vals[:n]), s0[:n], ln[:n], tg[:n], st[:n]
+
+
+def get_map_batch(arena, offsets, n: int, path, flags: int = MAP_STR, max_pairs: int = 8, stride: int = 0,
+                  stream=None):
+    """GetMapStr (flags=MAP_STR) / GetMapAny (MAP_ANY) of the map at `path`
+    over every blob (access/get.go:412-490): (pairs, key_start, key_len,
+    val_start, val_len, val_tag, status); the span tensors are (n, max_pairs),
+    pair j of blob i in wire order (GetMapOrderedAny's order).  status: 0 ok,
+    1 decode error, 2 nil nested accessor, 3 nil accessor (panic), 4 nil map,
+    5 more pairs than max_pairs, 6 nested deeper than 32 maps."""
+    torch = _torch()
+    dev = arena.device
+    m = max(max_pairs, 1)
+    pr = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    ks = torch.empty((max(n, 1), m), dtype=torch.int64, device=dev)
+    kl = torch.empty((max(n, 1), m), dtype=torch.int32, device=dev)
+    vs = torch.empty((max(n, 1), m), dtype=torch.int64, device=dev)
+    vl = torch.empty((max(n, 1), m), dtype=torch.int32, device=dev)
+    vt = torch.empty((max(n, 1), m), dtype=torch.uint8, device=dev)
+    st = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    p = (C.c_int32 * len(path))(*path)
+    check(lib().packos_get_map_batch(arena.data_ptr(), None if offsets is None else offsets.data_ptr(), stride, n,
+                                     p, len(path), flags, max_pairs, pr.data_ptr(), ks.data_ptr(), kl.data_ptr(),
+                                     vs.data_ptr(), vl.data_ptr(), vt.data_ptr(), st.data_ptr(), _stream_ptr(stream)),
+          "packos_get_map_batch")
+    mp = max_pairs
+    return pr[:n], ks[:n, :mp], kl[:n, :mp], vs[:n, :mp], vl[:n, :mp], vt[:n, :mp], st[:n]

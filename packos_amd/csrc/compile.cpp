@@ -231,7 +231,11 @@ struct Builder {
             Node& n = s->nodes[id];
             n.kind = K_BYTES; n.width = w > 0 ? w : -1; n.nullable = n.width <= 0;
         } else if (t == "tuple") {
-            if (bool_field(j, "flatten")) fail(PACKOS_E_UNSUPPORTED, "flattened tuples are outside the compiled subset");
+            // "flatten" (with variableLength: STupleValFlatten / STupleNamedValFlattened,
+            // schemabuilder_json.go:247-258) only changes how SRepeatSchema
+            // children encode and decode (schema.go:1616-1623,1649-1664,1781-1790,
+            // 1816); repeat is rejected below, so a flattened tuple is compiled
+            // exactly as the plain one
             const JVal* sch = j.get("schema");
             const JVal* names = j.get("fieldNames");
             {
@@ -956,6 +960,7 @@ int packos_schema_column_info(const packos_schema* s, int col, packos_column_inf
 }
 
 int packos_schema_decode_fast(const packos_schema* s) { return s && s->dec_fast == 1 ? 1 : 0; }
+int packos_schema_has_checks(const packos_schema* s) { return s && !s->echk.empty() ? 1 : 0; }
 
 int64_t packos_schema_fixed_blob_size(const packos_schema* s) {
     if (!s || s->has_var) return -1;

@@ -72,6 +72,10 @@ extern "C" int packos_encode_host_batch(const packos_schema* cs, const packos_co
                                         uint32_t* host_status, size_t chunk_blobs) {
     packos_schema* s = const_cast<packos_schema*>(cs);
     if (!s || !hc || (!host_out && n)) { set_error("packos_encode_host_batch: bad argument"); return PACKOS_E_INVALID; }
+    if (!host_status && !s->echk.empty()) {
+        set_error("packos_encode_host_batch: the schema has value checks: host_status required");
+        return PACKOS_E_INVALID;
+    }
     if (n == 0) {
         if (host_offsets) host_offsets[0] = 0;
         return PACKOS_OK;

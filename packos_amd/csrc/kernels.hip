@@ -523,7 +523,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_var(EncProgram P, EncCols col
 // failing check in emission order wins (EncodeValue stops there); values
 // inside a nil container or nil themselves are not encoded, so not checked.
 // Passing blobs are not touched; a failing blob's status becomes ErrEncode at
-// its top-level field with the leaf's code in bits 24..29.
+// position -1 with the leaf's code in bits 24..29.
 __global__ __launch_bounds__(kBlock) void k_encode_checks(const EncCheck* __restrict__ chk, int nchk, EncProgram P,
                                                           EncCols cols, uint64_t n, uint32_t* __restrict__ status,
                                                           int need_pm) {
@@ -559,8 +559,10 @@ __global__ __launch_bounds__(kBlock) void k_encode_checks(const EncCheck* __rest
             for (uint32_t b = 0; !bad && b < c.lit_len; b++) bad = p[at + b] != P.lits[c.lit + b];
         }
         if (bad) {
+            // position -1 (bits 8..23 = 0): EncodeValue wraps every leaf error as
+            // SchemaError(ErrEncode, ChainName, "", -1, err) (schema/schema.go:919-936)
             status[i] = (status[i] & (PACKOS_STATUS_PANIC | PACKOS_STATUS_OVERFLOW13)) | (uint32_t)PACKOS_ERR_ENCODE |
-                        ((uint32_t)(c.top + 1) << 8) | (c.inner << 24);
+                        (c.inner << 24);
             return;
         }
     }
@@ -1352,6 +1354,9 @@ __global__ __launch_bounds__(kBlock) void k_get_field(const uint8_t* __restrict_
             rc = tp != PACKOS_TAG_INTEGER ? 1 : w == 0 ? 4 : (w != 1 && w != 2 && w != 4 && w != 8);
             break;
         case PACKOS_GET_FLOAT: rc = tp != PACKOS_TAG_FLOATING ? 1 : w == 0 ? 4 : (w != 4 && w != 8); break;
+        case PACKOS_GET_ANY:   // GetTypeAndValue (get.go:504-510); past argCount buf[-2:-1] panics
+            rc = s < 0 ? 3 : e < s ? 1 : 0;
+            break;
         default: rc = 1;
     }
     status[i] = (uint8_t)rc;
@@ -1359,7 +1364,7 @@ __global__ __launch_bounds__(kBlock) void k_get_field(const uint8_t* __restrict_
     const uint64_t at = g.start + (uint64_t)s;
     out_start[i] = at;
     out_len[i] = (uint32_t)w;
-    if (!dst || getter == PACKOS_GET_SPAN) return;
+    if (!dst || getter == PACKOS_GET_SPAN || getter == PACKOS_GET_ANY) return;
     if (getter == PACKOS_GET_INT) {
         uint64_t v = 0;
         for (int k = 0; k < w; k++) v |= (uint64_t)r.byte(at + k) << (8 * k);
@@ -1370,6 +1375,147 @@ __global__ __launch_bounds__(kBlock) void k_get_field(const uint8_t* __restrict_
     } else {
         for (int64_t k = 0; k < w && k < (int64_t)value_width; k++) dst[k] = (uint8_t)r.byte(at + k);
     }
+}
+
+// GetMapStr / GetMapAny (get.go:412-490), one thread per blob: walk the path
+// like k_get_field, open the map, then validate every key (GetString) and
+// value (GetString, or GetAny with nested maps walked depth first on a small
+// explicit stack: the reference's GetMapAny -> GetAny recursion, get.go:377-
+// 436) in wire order, writing the first max_pairs top-level pairs' spans.
+constexpr int kMapDepth = 32;
+struct MapFrame {
+    DGet g;
+    int64_t j;
+};
+// GetAny of value position pos of map m (get.go:377-410): 0 ok, 1 error,
+// 3 panic (nil accessor), 7 = descend into `child` (a non-empty nested map)
+__device__ __forceinline__ int map_value(const DGet& m, const GWin& r, int64_t pos, bool any, bool xmode, DGet& child) {
+    int tp; int64_t s, e;
+    dget_range(m, r, pos, tp, s, e);
+    if (!any) return (e < s || tp != PACKOS_TAG_STRING) ? 1 : 0;   // GetString (get.go:359-365)
+    if (pos >= m.argc) return 1;   // GetAny reads the End header; every getter then fails
+    const int64_t w = e - s;
+    switch (tp) {
+        case PACKOS_TAG_INTEGER: return (w == 0 || w == 1 || w == 2 || w == 4 || w == 8) ? 0 : 1;
+        case PACKOS_TAG_FLOATING: return (w == 0 || w == 4 || w == 8) ? 0 : 1;
+        case PACKOS_TAG_STRING: return e < s ? 1 : 0;
+        case PACKOS_TAG_MAP: case PACKOS_TAG_EXTENDED: {
+            const bool x = tp == PACKOS_TAG_EXTENDED;
+            if ((x && !xmode) || e < s) return 1;
+            if (e == s) return 0;   // nil map value
+            if (x) return dget_init_ext(child, r, m.start + (uint64_t)s, e - s, false) &&
+                                  r.u16(m.start + (uint64_t)s + 2) == PACKOS_TAG_MAP ? 7 : 1;
+            return dget_init(child, r, m.start + (uint64_t)s, e - s) ? 7 : 3;
+        }
+        default: return 1;   // "GetAny: unsupported type tag" (End, Tuple, Bool)
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_get_map(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
+                                                    uint64_t stride, uint64_t n, PathArg path, int depth, int flags,
+                                                    uint32_t max_pairs, uint32_t* __restrict__ out_pairs,
+                                                    uint64_t* __restrict__ key_start, uint32_t* __restrict__ key_len,
+                                                    uint64_t* __restrict__ val_start, uint32_t* __restrict__ val_len,
+                                                    uint8_t* __restrict__ val_tag, uint8_t* __restrict__ status) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t a0 = offs ? offs[i] : i * stride;
+    const uint64_t a1 = offs ? offs[i + 1] : (i + 1) * stride;
+    GWin r;
+    r.a = arena;
+    r.base = a0;
+    const uint64_t bl = a1 > a0 ? a1 - a0 : 0;
+    r.n = bl >= 32 ? 32u : bl >= 16 ? 16u : 0u;
+    {
+        const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+        const u32x4 w0 = r.n >= 16 ? *(const g_u32x4*)(arena + a0) : z;
+        const u32x4 w1 = r.n >= 32 ? *(const g_u32x4*)(arena + a0 + 16) : z;
+        r.W[0] = w0.x; r.W[1] = w0.y; r.W[2] = w0.z; r.W[3] = w0.w;
+        r.W[4] = w1.x; r.W[5] = w1.y; r.W[6] = w1.z; r.W[7] = w1.w;
+    }
+    out_pairs[i] = 0;
+    for (uint32_t j = 0; j < max_pairs; j++) {
+        const uint64_t k = i * max_pairs + j;
+        key_start[k] = 0; key_len[k] = 0; val_start[k] = 0; val_len[k] = 0; val_tag[k] = 0;
+    }
+    const bool xmode = (flags & PACKOS_GET_EXTENDED) != 0;
+    const bool any = (flags & ~PACKOS_GET_EXTENDED) == PACKOS_MAP_ANY;
+    DGet g;
+    const bool xtop = xmode && a1 - a0 >= 2 && r.u16(a0) == kExtMarker;
+    if (!(xtop ? dget_init_ext(g, r, a0, (int64_t)(a1 - a0), true) : dget_init(g, r, a0, (int64_t)(a1 - a0)))) {
+        status[i] = 3;
+        return;
+    }
+    int tp; int64_t s, e;
+    for (int d = 0; d < depth - 1; d++) {
+        dget_range(g, r, path.p[d], tp, s, e);
+        const bool x = xmode && tp == PACKOS_TAG_EXTENDED;
+        if (e < s || (tp != 7 && tp != 4 && !x)) { status[i] = 1; return; }
+        if (e == s) { status[i] = 2; return; }
+        DGet nx;
+        if (x) {
+            if (!dget_init_ext(nx, r, g.start + (uint64_t)s, e - s, false)) { status[i] = 1; return; }
+        } else if (!dget_init(nx, r, g.start + (uint64_t)s, e - s)) {
+            status[i] = 3;
+            return;
+        }
+        g = nx;
+    }
+    dget_range(g, r, path.p[depth - 1], tp, s, e);
+    const bool x = xmode && tp == PACKOS_TAG_EXTENDED;
+    if (e < s || (tp != PACKOS_TAG_MAP && !x)) { status[i] = 1; return; }   // get.go:414-416
+    if (e == s) { status[i] = 4; return; }                                    // nil map
+    MapFrame stk[kMapDepth];
+    int sp = 0;
+    if (x) {
+        if (!dget_init_ext(stk[0].g, r, g.start + (uint64_t)s, e - s, false) ||
+            r.u16(g.start + (uint64_t)s + 2) != PACKOS_TAG_MAP) { status[i] = 1; return; }
+    } else if (!dget_init(stk[0].g, r, g.start + (uint64_t)s, e - s)) {
+        status[i] = 3;
+        return;
+    }
+    stk[0].j = 0;
+    sp = 1;
+    uint32_t pairs = 0;
+    int rc = 0;
+    while (sp > 0) {
+        MapFrame& f = stk[sp - 1];
+        if (f.j >= f.g.argc) { sp--; continue; }
+        const int64_t j = f.j;
+        f.j += 2;
+        int kt; int64_t ks, ke;
+        dget_range(f.g, r, j, kt, ks, ke);   // key: GetString
+        if (ke < ks || kt != PACKOS_TAG_STRING) { rc = 1; break; }
+        DGet child;
+        const int v = map_value(f.g, r, j + 1, any, xmode, child);
+        if (sp == 1) {
+            if (v != 1 && v != 3 && pairs < max_pairs) {
+                int vt; int64_t vs, ve;
+                dget_range(f.g, r, j + 1, vt, vs, ve);
+                const uint64_t k = i * max_pairs + pairs;
+                key_start[k] = f.g.start + (uint64_t)ks; key_len[k] = (uint32_t)(ke - ks);
+                val_start[k] = f.g.start + (uint64_t)vs; val_len[k] = (uint32_t)(ve - vs); val_tag[k] = (uint8_t)vt;
+            }
+            pairs++;
+        }
+        if (v == 1 || v == 3) { rc = v; break; }
+        if (v == 7) {
+            if (sp >= kMapDepth) { rc = 6; break; }
+            stk[sp].g = child;
+            stk[sp].j = 0;
+            sp++;
+        }
+    }
+    if (rc) {
+        status[i] = (uint8_t)rc;
+        for (uint32_t j = 0; j < max_pairs && j < pairs; j++) {   // a failing call returns no map
+            const uint64_t k = i * max_pairs + j;
+            key_start[k] = 0; key_len[k] = 0; val_start[k] = 0; val_len[k] = 0; val_tag[k] = 0;
+        }
+        return;
+    }
+    out_pairs[i] = pairs;
+    status[i] = pairs > max_pairs ? 5 : 0;
 }
 
 // =========================================================================
@@ -1680,6 +1826,12 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
         if (out_offsets) HIP_TRY(hipMemsetAsync(out_offsets, 0, sizeof(uint64_t), (hipStream_t)stream));
         return PACKOS_OK;
     }
+    if (!status && !s->echk.empty()) {
+        // EncodeValue returns ErrEncode (and no bytes) for a failing value check:
+        // without a status array the failure could not be reported
+        set_error("packos_encode_batch: the schema has value checks (Range / date / prefix / suffix): status required");
+        return PACKOS_E_INVALID;
+    }
     int dev, r;
     if ((r = current_device(&dev))) return r;
     DeviceTables* t;
@@ -1690,7 +1842,7 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
     hipStream_t st = (hipStream_t)stream;
     if ((r = encode_batch_impl(s, t, ec, any_nil, n, out, cap, out_offsets, status, ws, ws_bytes, flags, st)))
         return r;
-    if (status && !s->echk.empty()) {
+    if (!s->echk.empty()) {
         bool pm = false;
         for (const EncCont& c : s->conts) pm = pm || (c.valid_col >= 0 && ec.valid[c.valid_col]);
         hipLaunchKernelGGL(k_encode_checks, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, t->echk,
@@ -1959,7 +2111,7 @@ int packos_get_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t str
     if (!path || depth < 1 || depth > 16 || !out_start || !out_len || !out_tag || !status || (!arena && n))
         return PACKOS_E_INVALID;
     const int g_base = getter & ~PACKOS_GET_EXTENDED;
-    if (g_base < PACKOS_GET_FIXED || g_base > PACKOS_GET_FLOAT) {
+    if (g_base < PACKOS_GET_FIXED || g_base > PACKOS_GET_ANY) {
         set_error("unknown getter");
         return PACKOS_E_INVALID;
     }
@@ -1979,6 +2131,33 @@ int packos_get_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t str
     hipLaunchKernelGGL(k_get_field, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        (hipStream_t)stream, arena, offsets, stride, (uint64_t)n, pa, depth, getter, want_tag,
                        want_width, out_values, value_width, out_start, out_len, out_tag, status);
+    HIP_TRY(hipGetLastError());
+    return PACKOS_OK;
+}
+
+int packos_get_map_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride, size_t n, const int32_t* path,
+                         int depth, int flags, uint32_t max_pairs, uint32_t* out_pairs, uint64_t* key_start,
+                         uint32_t* key_len, uint64_t* val_start, uint32_t* val_len, uint8_t* val_tag, uint8_t* status,
+                         void* stream) {
+    if (!path || depth < 1 || depth > 16 || !out_pairs || !status || (!arena && n)) return PACKOS_E_INVALID;
+    const int f = flags & ~PACKOS_GET_EXTENDED;
+    if (f != PACKOS_MAP_STR && f != PACKOS_MAP_ANY) { set_error("unknown map getter"); return PACKOS_E_INVALID; }
+    if (max_pairs && (!key_start || !key_len || !val_start || !val_len || !val_tag)) {
+        set_error("max_pairs > 0 needs the key / value span arrays");
+        return PACKOS_E_INVALID;
+    }
+    if (n == 0) return PACKOS_OK;
+    if (!offsets && stride == 0) return PACKOS_E_INVALID;
+    int dev, r;
+    if ((r = current_device(&dev))) return r;
+    PathArg pa{};
+    for (int d = 0; d < depth; d++) {
+        if (path[d] < 0) { set_error("negative field position"); return PACKOS_E_INVALID; }
+        pa.p[d] = path[d];
+    }
+    hipLaunchKernelGGL(k_get_map, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, (hipStream_t)stream,
+                       arena, offsets, stride, (uint64_t)n, pa, depth, flags, max_pairs, out_pairs, key_start, key_len,
+                       val_start, val_len, val_tag, status);
     HIP_TRY(hipGetLastError());
     return PACKOS_OK;
 }

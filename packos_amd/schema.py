@@ -39,6 +39,7 @@ __all__ = [
     "SNullFloat32", "SNullFloat64", "SNullUint8", "SNullUint16", "SNullUint32", "SNullUint64",
     "SString", "SStringLen", "SStringExact", "SVariableString", "SBytes", "SVariableBytes",
     "SMap", "SMapSorted", "SVariableMap", "STuple", "STupleVal", "STupleNamed", "STupleNamedVal",
+    "STupleValFlatten", "STupleNamedValFlattened",
     "SDateRange", "BuildSchema", "TAG_OF_KIND",
     "CHK_MIN", "CHK_MAX", "CHK_DATE", "CHK_PREFIX", "CHK_SUFFIX", "CHK_DEFAULT",
 ]
@@ -125,6 +126,7 @@ class Schema:
     rmax: int = 0
     check_lit: bytes = b""
     default: bytes = b""
+    flatten: bool = False   # STupleValFlatten / STupleNamedValFlattened (only SRepeatSchema children differ)
 
     # -- value checks (schema/schema.go:1131-1364, 2188-2250) ------------------
     def Range(self, min=None, max=None) -> "Schema":
@@ -268,6 +270,8 @@ class Schema:
                 d["fieldNames"] = list(self.names)
             if self.variable:
                 d["variableLength"] = True
+            if self.flatten:
+                d["flatten"] = True
             return d
         if k == "map":
             d = {"type": "map", "schema": [c.to_json() for c in self.children]}
@@ -353,6 +357,19 @@ def STuple(*schemas: Schema) -> Schema:
 
 def STupleVal(*schemas: Schema) -> Schema:
     return Schema("tuple", nullable=True, children=tuple(schemas), variable=True)
+
+
+def STupleValFlatten(*schemas: Schema) -> Schema:
+    """STupleValFlatten (schema/schema.go:1559-1561).  Flatten changes only how
+    SRepeatSchema children encode / decode (:1616-1623, :1649-1664), and repeat
+    is outside the compiled subset, so the bytes are STupleVal's."""
+    return Schema("tuple", nullable=True, children=tuple(schemas), variable=True, flatten=True)
+
+
+def STupleNamedValFlattened(names: Sequence[str], *schemas: Schema) -> Schema:
+    """STupleNamedValFlattened (schema/schema.go:1711-1719); see STupleValFlatten."""
+    return Schema("tuple", nullable=True, children=tuple(schemas), names=tuple(names), variable=True,
+                  flatten=True)
 
 
 def STupleNamed(names: Optional[Sequence[str]], *schemas: Schema) -> Schema:
@@ -466,11 +483,13 @@ def BuildSchema(js) -> Schema:
         kids = [BuildSchema(c) for c in js.get("schema", [])]
         names = js.get("fieldNames")
         var = bool(js.get("variableLength", False))
-        if js.get("flatten"):
-            raise NotImplementedError("flatten/repeat is outside the compiled subset")
+        # "flatten" counts only with variableLength (schemabuilder_json.go:247-258):
+        # STupleValFlatten / STupleNamedValFlattened, byte-identical to the
+        # non-flattened forms without SRepeatSchema children (rejected here)
+        flat = var and bool(js.get("flatten", False))
         # every STuple* is Nullable: true; BuildSchema never reads the key
         node = Schema("tuple", nullable=True, children=tuple(kids),
-                      names=tuple(names) if names else None, variable=var)
+                      names=tuple(names) if names else None, variable=var, flatten=flat)
         return node
     if t == "map":
         kids = [BuildSchema(c) for c in js.get("schema", [])]

@@ -226,6 +226,21 @@ GET = [
         ([1, 3], 6, -1, b"gopher".hex())]),
 ]
 
+# map-walk known answers (GetMapStr / GetMapAny / GetMapOrderedAny): (id,
+# source, bytes, path, flags 0 = MAP_STR / 1 = MAP_ANY, expected pairs in wire
+# order as (key, value tag, value payload))
+INNER_MAP = bytes([0x56, 0x00, 0x26, 0x00, 0x4E, 0x00, 0x6E, 0x00, 0x90, 0x00]) + b"roleadminuseralice"
+MAPS = [
+    ("map_str", "access/get_test.go:46-63 (GetMapStr(0) == {role: admin, user: alice})",
+     ("access/get_test.go", 47), [0], 0, [(b"role", 6, b"admin"), (b"user", 6, b"alice")]),
+    ("map_ordered_any", "access/get_test.go:65-96 (GetMapOrderedAny(0): role, user in order)",
+     ("access/get_test.go", 66), [0], 1, [(b"role", 6, b"admin"), (b"user", 6, b"alice")]),
+    ("map_any_nested", "access/get_test.go:98-126 (GetMapAny(1): meta -> map, name -> gopher)",
+     ("access/get_test.go", 99), [1], 1, [(b"meta", 7, INNER_MAP), (b"name", 6, b"gopher")]),
+    ("map_any_inner", "access/get_test.go:98-126 (m[\"meta\"]: role -> admin, user -> alice)",
+     ("access/get_test.go", 99), [1, 1], 1, [(b"role", 6, b"admin"), (b"user", 6, b"alice")]),
+]
+
 SEQ = [
     ("seq_nested_map", "access/seqget_test.go:11-101", ("access/seqget_test.go", 12)),
     ("seq_flat_end", "access/seqget_test.go:103-151", ("access/seqget_test.go", 104)),
@@ -293,7 +308,7 @@ DECODE = [
 def main():
     if not os.path.isdir(REF):
         sys.exit("reference not present; vectors.json is already committed")
-    out = {"note": __doc__.strip().split("\n")[0], "encode": [], "equal": [], "get": [], "seq": [],
+    out = {"note": __doc__.strip().split("\n")[0], "encode": [], "equal": [], "get": [], "maps": [], "seq": [],
            "inputs": [], "decode": []}
     for cid, src, mode, schema, row, (bf, bl) in ENCODE:
         out["encode"].append({"id": cid, "source": src, "mode": mode, "schema": schema, "row": row,
@@ -306,6 +321,10 @@ def main():
                            "hex": extract_bytes(bf, bl).hex(),
                            "queries": [{"path": p, "tag": t, "width": w, "expect": e}
                                        for p, t, w, e in queries]})
+    for cid, src, (bf, bl), path, flags, pairs in MAPS:
+        out["maps"].append({"id": cid, "source": src, "bytes_from": f"{bf}:{bl}",
+                            "hex": extract_bytes(bf, bl).hex(), "path": path, "flags": flags,
+                            "pairs": [[k.hex(), t, v.hex()] for k, t, v in pairs]})
     for cid, src, (bf, bl) in SEQ:
         out["seq"].append({"id": cid, "source": src, "bytes_from": f"{bf}:{bl}",
                            "hex": extract_bytes(bf, bl).hex()})
@@ -317,7 +336,7 @@ def main():
     with open(OUT, "w") as f:
         json.dump(out, f, indent=1)
     print(f"wrote {OUT}: {len(out['encode'])} encode, {len(out['equal'])} equal, "
-          f"{len(out['get'])} get, {len(out['seq'])} seq, {len(out['inputs'])} inputs, {len(out['decode'])} decode")
+          f"{len(out['get'])} get, {len(out['maps'])} maps, {len(out['seq'])} seq, {len(out['inputs'])} inputs, {len(out['decode'])} decode")
 
 
 if __name__ == "__main__":

@@ -91,6 +91,9 @@ def lib():
         L.or_get_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_size_t, C.c_void_p,
                                    C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_uint32,
                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.or_get_map_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_size_t, C.c_void_p, C.c_int,
+                                       C.c_int, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -258,7 +261,7 @@ def get_batch(arena, offsets, n, path, getter, want_tag=0, want_width=0, stride=
     p = np.asarray(path, dtype=np.int32)
     fam = getter & 0xFF
     vw = 8 if fam in (3, 4) else max(want_width, 0)
-    gather = values and fam != 2 and vw > 0
+    gather = values and fam not in (2, 5) and vw > 0
     vals = np.zeros((max(n, 1), vw), np.uint8) if gather else None
     s0 = np.zeros(max(n, 1), np.uint64)
     ln = np.zeros(max(n, 1), np.uint32)
@@ -267,6 +270,27 @@ def get_batch(arena, offsets, n, path, getter, want_tag=0, want_width=0, stride=
     lib().or_get_batch(_ptr(a), _ptr(o), stride, n, _ptr(p), len(path), getter, want_tag, want_width,
                        _ptr(vals), vw if gather else 0, _ptr(s0), _ptr(ln), _ptr(tg), _ptr(st))
     return (None if vals is None else vals[:n]), s0[:n], ln[:n], tg[:n], st[:n]
+
+
+def get_map_batch(arena, offsets, n, path, flags, max_pairs, stride=0):
+    """or_get_map_batch: (pairs, key_start, key_len, val_start, val_len,
+    val_tag, status) with (n, max_pairs) span arrays, the contract of
+    packos_amd.api.get_map_batch."""
+    a = np.ascontiguousarray(arena, dtype=np.uint8)
+    if a.size == 0:
+        a = np.zeros(1, np.uint8)
+    o = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+    p = np.asarray(path, dtype=np.int32)
+    m = max(max_pairs, 1)
+    pr = np.zeros(max(n, 1), np.uint32)
+    ks, kl = np.zeros((max(n, 1), m), np.uint64), np.zeros((max(n, 1), m), np.uint32)
+    vs, vl = np.zeros((max(n, 1), m), np.uint64), np.zeros((max(n, 1), m), np.uint32)
+    vt = np.zeros((max(n, 1), m), np.uint8)
+    st = np.zeros(max(n, 1), np.uint8)
+    lib().or_get_map_batch(_ptr(a), _ptr(o), stride, n, _ptr(p), len(path), flags, max_pairs, _ptr(pr), _ptr(ks),
+                           _ptr(kl), _ptr(vs), _ptr(vl), _ptr(vt), _ptr(st))
+    mp = max_pairs
+    return pr[:n], ks[:n, :mp], kl[:n, :mp], vs[:n, :mp], vl[:n, :mp], vt[:n, :mp], st[:n]
 
 
 # ---- single-buffer GetAccess / SeqGetAccess wrappers (golden decode tests) ----

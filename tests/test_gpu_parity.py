@@ -12,7 +12,8 @@ import pytest
 import oracle_bridge as ob
 from packos_amd import _lib
 from golden_util import MODES, chain_of, load, unwrap
-from packos_amd.api import CompiledSchema, DeviceColumns, decode_batch, encode_batch, get_batch, get_field_batch
+from packos_amd.api import (CompiledSchema, DeviceColumns, decode_batch, encode_batch, get_batch, get_field_batch,
+                           get_map_batch)
 from packos_amd.columns import HostColumns
 from packos_amd.configs import CONFIGS, make_columns
 from packos_amd.schema import SBool, SChain, SInt16, SInt32, SInt64, SStringLen, SVariableString, STuple, SMap, SString
@@ -811,7 +812,7 @@ def test_random_get(seed):
 
 GETTERS = [(0, 1, 1), (0, 1, 2), (0, 1, 4), (0, 1, 8), (0, 3, 4), (0, 3, 8), (0, 5, 1),
            (1, 1, 4), (1, 1, 8), (1, 3, 8), (1, 5, 1), (2, 6, 0), (2, 4, 0), (2, 7, 0),
-           (3, 0, 0), (4, 0, 0)]
+           (3, 0, 0), (4, 0, 0), (5, 0, 0)]
 
 
 @pytest.mark.parametrize("seed", range(16))
@@ -865,6 +866,86 @@ def test_get_batch_nullable_and_any_width():
         assert np.array_equal(o[4], g[4].cpu().numpy())
         if o[0] is not None:
             assert np.array_equal(o[0], g[0].cpu().numpy())
+
+
+def _rand_map_value(rng, depth):
+    """(tag, payload) of a random GetAny-relevant value: ints of legal and
+    illegal widths, floats, strings, bools, tuples, nil / nested maps."""
+    from test_oracle_golden import pack_fields
+    k = int(rng.integers(0, 10))
+    if k < 3:
+        return 1, bytes(rng.integers(0, 256, int(rng.choice([0, 1, 2, 3, 4, 8])), dtype=np.uint8))
+    if k == 3:
+        return 3, bytes(rng.integers(0, 256, int(rng.choice([0, 4, 8, 2])), dtype=np.uint8))
+    if k < 6:
+        return 6, bytes(rng.integers(97, 123, int(rng.integers(0, 12)), dtype=np.uint8))
+    if k == 6:
+        return int(rng.choice([5, 4])), b"\x01"
+    if depth >= 3 or k == 7:
+        return 7, b""
+    return 7, _rand_map(rng, depth + 1)
+
+
+def _rand_map(rng, depth=0):
+    from test_oracle_golden import pack_fields
+    fields = []
+    for _ in range(int(rng.integers(0, 5))):
+        fields.append((6 if rng.random() > 0.05 else 1, bytes(rng.integers(97, 123, int(rng.integers(1, 6)),
+                                                                               dtype=np.uint8))))
+        fields.append(_rand_map_value(rng, depth))
+    if rng.random() < 0.05 and fields:
+        fields.pop()   # odd field count
+    return pack_fields(fields)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_get_map_batch(seed):
+    """packos_get_map_batch vs or_get_map_batch (GetMapStr / GetMapAny) on
+    random blobs holding maps of mixed values (nested maps, bools, tuples,
+    illegal int widths, nil maps), a fifth of the blobs corrupted."""
+    from test_oracle_golden import pack_fields
+    T = torch()
+    rng = np.random.default_rng(700 + seed)
+    blobs = []
+    for i in range(2000):
+        fields = [(1, b"\x01\x00"), (7, _rand_map(rng)), (4, pack_fields([(7, _rand_map(rng))]))]
+        b = bytearray(pack_fields(fields))
+        if i % 5 == 0 and b:
+            b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
+        blobs.append(bytes(b))
+    offs = np.zeros(len(blobs) + 1, np.uint64)
+    np.cumsum([len(b) for b in blobs], out=offs[1:])
+    arena = np.frombuffer(b"".join(blobs), np.uint8).copy()
+    da = T.from_numpy(arena).to("cuda:0")
+    do = T.from_numpy(offs.astype(np.int64)).to("cuda:0")
+    for path in ([1], [2, 0], [0], [3]):
+        for flags in (0, 1):
+            for mp in (0, 2, 8):
+                o = ob.get_map_batch(arena, offs, len(blobs), path, flags, mp)
+                g = [x.cpu().numpy() for x in get_map_batch(da, do, len(blobs), path, flags, mp)]
+                what = (path, flags, mp)
+                assert np.array_equal(o[6], g[6]), what
+                assert np.array_equal(o[0], g[0].astype(np.uint32)), what
+                for a, b_ in zip(o[1:6], g[1:6]):
+                    assert np.array_equal(a, b_.astype(a.dtype)), what
+    st = ob.get_map_batch(arena, offs, len(blobs), [1], 1, 8)[6]
+    assert len(set(st.tolist())) >= 3   # the mix exercises ok, error and nil-map outcomes
+
+
+def test_get_map_golden():
+    """The reference's map known answers (access/get_test.go:46-126) on the GPU."""
+    T = torch()
+    for c in G["maps"]:
+        buf = np.frombuffer(bytes.fromhex(c["hex"]), np.uint8)
+        reps = np.concatenate([buf] * 3)
+        da = T.from_numpy(reps).to("cuda:0")
+        pr, ks, kl, vs, vl, vt, st = [x.cpu().numpy() for x in
+                                      get_map_batch(da, None, 3, c["path"], c["flags"], 4, stride=buf.size)]
+        for i in range(3):
+            assert st[i] == 0 and pr[i] == len(c["pairs"]), c["id"]
+            got = [(bytes(reps[int(ks[i, j]):int(ks[i, j]) + int(kl[i, j])]).hex(), int(vt[i, j]),
+                    bytes(reps[int(vs[i, j]):int(vs[i, j]) + int(vl[i, j])]).hex()) for j in range(pr[i])]
+            assert got == [tuple(p) for p in c["pairs"]], c["id"]
 
 
 def _blob_with_nils():

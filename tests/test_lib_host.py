@@ -142,3 +142,31 @@ def test_rfc3339_dates():
         s = CompiledSchema(json.dumps([{"type": "date", "dateFrom": txt, "dateTo": txt}]))
         line = next(l for l in s.describe().split("\n") if l.startswith("check "))
         assert f"min={unix} max={unix}" in line, (txt, line)
+
+
+def test_flatten_tuple_compiles_as_plain():
+    """BuildSchema's "flatten" (STupleValFlatten / STupleNamedValFlattened,
+    schemabuilder_json.go:247-258) differs from the plain variable tuple only
+    for SRepeatSchema children (schema.go:1616-1623): same compiled layout."""
+    from packos_amd.schema import BuildChain
+    kids = [{"type": "int32"}, {"type": "string"}, {"type": "bytes", "width": 4}]
+    for named in (False, True):
+        base = {"type": "tuple", "schema": kids, "variableLength": True}
+        if named:
+            base["fieldNames"] = ["a", "b", "c"]
+        flat = dict(base, flatten=True)
+        js_plain, js_flat = json.dumps([{"type": "int16"}, base]), json.dumps([{"type": "int16"}, flat])
+        a, b = CompiledSchema(js_plain), CompiledSchema(js_flat)
+        assert a.describe() == b.describe()
+        assert BuildChain(js_flat).Schemas[1].flatten and b.chain.to_json()[1]["flatten"] is True
+    # without variableLength, BuildSchema ignores "flatten" (plain STuple)
+    js = json.dumps([{"type": "tuple", "schema": kids, "flatten": True}])
+    assert not BuildChain(js).Schemas[0].flatten
+    assert CompiledSchema(js).describe() == CompiledSchema(json.dumps([{"type": "tuple", "schema": kids}])).describe()
+
+
+def test_has_checks():
+    assert not CompiledSchema(CONFIGS["M"].chain).has_checks
+    assert CompiledSchema(json.dumps([{"type": "int16", "min": 0, "max": 9}])).has_checks
+    assert CompiledSchema(json.dumps([{"type": "string", "prefix": "ab"}])).has_checks
+    assert not CompiledSchema(json.dumps([{"type": "string", "decodeDefault": "x"}])).has_checks

@@ -85,15 +85,17 @@ def test_ranks_encode_disjoint_shards(cfg_name, per_gpu, world):
 def test_bench_two_ranks_rehearsal():
     """bench.py under torch.distributed.run with 2 ranks (both on cuda:0,
     gloo for the barrier / timing all-reduce): one JSON line, n_gpus = 2,
-    the global batch = 2 x per-GPU blobs."""
+    the global batch = 2 x per-GPU blobs, per-rank oracle parity."""
     env = dict(os.environ, PACKOS_BENCH_DEVICE="0", PACKOS_BENCH_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--config", "C5", "--blobs-per-gpu", "20000", "--steps", "3", "--warmup", "1", "--sets", "1",
-           "--no-cpu", "--no-host", "--no-warm"]
+           "--no-host", "--no-warm"]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["config"]["global_blobs"] == 40000 and line["value"] > 0
+    # every rank checked its shard against the oracle's encoding of its slice
+    assert line["parity"]["result"] == "bit-exact" and line["parity"]["ranks"] == 2

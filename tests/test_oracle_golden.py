@@ -117,6 +117,75 @@ def test_get_batch_getters(path, getter, tag, width, status, value):
         assert bytes(buf[int(s0[0]):int(s0[0]) + int(ln[0])]) == b"abc"
 
 
+@pytest.mark.parametrize("path,status,tag,payload", [
+    ([0], 0, 1, (-300).to_bytes(2, "little", signed=True)),   # GetTypeAndValue: any tag
+    ([1], 0, 1, b""),                                          # nil value: empty, not invalid
+    ([4], 0, 6, b"abc"),
+    ([9], 3, 0, None),                                         # past argCount: buf[-2:-1] panics
+])
+def test_get_any_type_and_value(path, status, tag, payload):
+    """GetTypeAndValue (access/get.go:504-510): (tag, buf[start:end]) for any
+    tag; TypeInvalid + nil only when end < start (derived: no reference test
+    calls it)."""
+    blob = pack_fields(NIL_FIELDS)
+    buf = np.frombuffer(blob, np.uint8)
+    vals, s0, ln, tg, st = ob.get_batch(buf, np.asarray([0, len(blob)], np.uint64), 1, path, 5)
+    assert vals is None and st[0] == status and tg[0] == tag
+    if payload is not None:
+        assert bytes(buf[int(s0[0]):int(s0[0]) + int(ln[0])]) == payload
+
+
+@pytest.mark.parametrize("case", [c["id"] for c in G["maps"]])
+def test_map_getters_golden(case):
+    """GetMapStr / GetMapAny / GetMapOrderedAny known answers of
+    access/get_test.go (pairs in wire order, nested map values as spans)."""
+    c = next(x for x in G["maps"] if x["id"] == case)
+    buf = np.frombuffer(bytes.fromhex(c["hex"]), np.uint8)
+    offs = np.asarray([0, buf.size], np.uint64)
+    pr, ks, kl, vs, vl, vt, st = ob.get_map_batch(buf, offs, 1, c["path"], c["flags"], 4)
+    assert st[0] == 0 and pr[0] == len(c["pairs"])
+    got = [(bytes(buf[int(ks[0, j]):int(ks[0, j]) + int(kl[0, j])]).hex(), int(vt[0, j]),
+            bytes(buf[int(vs[0, j]):int(vs[0, j]) + int(vl[0, j])]).hex()) for j in range(pr[0])]
+    assert got == [tuple(p) for p in c["pairs"]]
+    # max_pairs smaller than the map: the first pairs, status 5
+    pr, ks, kl, vs, vl, vt, st = ob.get_map_batch(buf, offs, 1, c["path"], c["flags"], 1)
+    assert st[0] == 5 and pr[0] == len(c["pairs"])
+
+
+def _map(pairs):
+    """A map container of (key bytes, tag, value bytes) pairs."""
+    fields = []
+    for k, t, v in pairs:
+        fields += [(6, k), (t, v)]
+    return pack_fields(fields)
+
+
+@pytest.mark.parametrize("name,blob,flags,status", [
+    # GetMapStr needs String values; GetMapAny takes ints / floats / nested maps
+    ("str_int_value", pack_fields([(7, _map([(b"a", 1, b"\x01\x00")]))]), 0, 1),
+    ("any_int_value", pack_fields([(7, _map([(b"a", 1, b"\x01\x00")]))]), 1, 0),
+    ("any_int3_value", pack_fields([(7, _map([(b"a", 1, b"\x01\x00\x00")]))]), 1, 1),
+    ("any_nil_float", pack_fields([(7, _map([(b"a", 3, b"")]))]), 1, 0),
+    ("any_bool_value", pack_fields([(7, _map([(b"a", 5, b"\x01")]))]), 1, 1),     # GetAny has no Bool case
+    ("any_tuple_value", pack_fields([(7, _map([(b"a", 4, _map([]))]))]), 1, 1),
+    ("any_nested_bad", pack_fields([(7, _map([(b"a", 7, _map([(b"k", 5, b"\x00")]))]))]), 1, 1),
+    ("any_nested_nil", pack_fields([(7, _map([(b"a", 7, b"")]))]), 1, 0),
+    ("key_not_string", pack_fields([(7, pack_fields([(1, b"\x01"), (6, b"v")]))]), 0, 1),
+    ("odd_fields", pack_fields([(7, pack_fields([(6, b"k")]))]), 1, 1),
+    ("nil_map", pack_fields([(7, b"")]), 0, 4),
+    ("not_a_map", pack_fields([(4, _map([]))]), 0, 1),
+    ("nested_short", pack_fields([(7, b"\x40\x00")]), 0, 3),   # NewGetAccess -> nil: panic
+])
+def test_map_getters_rules(name, blob, flags, status):
+    """Derived from access/get.go:377-490 (GetAny's tag switch, GetMapStr's
+    GetString on keys and values, nil map / nil accessor)."""
+    buf = np.frombuffer(blob, np.uint8)
+    pr, ks, kl, vs, vl, vt, st = ob.get_map_batch(buf, np.asarray([0, buf.size], np.uint64), 1, [0], flags, 2)
+    assert st[0] == status, name
+    if status:
+        assert int(ks.sum()) == 0 and int(vl.sum()) == 0
+
+
 def test_seqget_nested_map_golden():
     # access/seqget_test.go:11-101
     case = next(c for c in G["seq"] if c["id"] == "seq_nested_map")
