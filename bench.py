@@ -207,12 +207,46 @@ def shard_parity(cfg, hc, gpu_arena, gpu_offsets, threads):
     return same, hashlib.sha256(gpu_arena[:total].tobytes()).hexdigest()[:16]
 
 
-def host_leg(schema, hc):
-    """packos_encode_host_batch: pinned host columns -> chunked H2D / encode /
+def pcie_ceiling(dev, nbytes=256 << 20, reps=5):
+    """Pinned host <-> device copy rates of this box (GB/s): H2D alone, D2H
+    alone, and both at once on two streams (the full-duplex ceiling a
+    pipelined host batch can reach)."""
+    import torch
+    h_in = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    h_out = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    d_in = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    d_out = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def run(h2d, d2h):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            if h2d:
+                with torch.cuda.stream(s1):
+                    d_in.copy_(h_in, non_blocking=True)
+            if d2h:
+                with torch.cuda.stream(s2):
+                    h_out.copy_(d_out, non_blocking=True)
+        torch.cuda.synchronize()
+        return nbytes * reps / (time.perf_counter() - t0) / 1e9
+    run(True, True)
+    h2d, d2h = run(True, False), run(False, True)
+    both = run(True, True)
+    return {"h2d_gbs": round(h2d, 2), "d2h_gbs": round(d2h, 2), "bidir_each_gbs": round(both, 2),
+            "note": f"pinned torch copies of {nbytes >> 20} MiB x {reps}; bidir = H2D and D2H on two streams at once"}
+
+
+def host_leg(schema, hc, dev):
+    """packos_encode_host_batch: pinned host columns -> pipelined H2D / encode /
     D2H through the library (the entry point a cgo shim binds) -> pinned host
-    arena.  Best of 3; never `value`."""
+    arena, and packos_decode_host_batch back.  Best of 2 per chunk size after
+    one warm-up call (the schema's cached pipeline keeps its buffers); never
+    `value`.  `frac_of_pcie` = the time the bytes need at the box's measured
+    full-duplex copy rates / the measured time."""
     import torch
     from packos_amd.api import encode_host_batch, host_batch_bound
+    pcie = pcie_ceiling(dev)
     pinned = []
     for lst in (hc.data, hc.offsets, hc.valid):
         for c, a in enumerate(lst):
@@ -224,7 +258,8 @@ def host_leg(schema, hc):
     out = torch.empty(cap, dtype=torch.uint8).pin_memory().numpy()
     offs = torch.empty(hc.n + 1, dtype=torch.int64).pin_memory().numpy().view(np.uint64)
     best = None
-    for chunk in (1 << 18, 1 << 20):
+    encode_host_batch(schema, hc, chunk_blobs=1 << 17, want_status=False, out=out, offsets=offs)   # warm-up
+    for chunk in (1 << 15, 1 << 16, 1 << 17, 1 << 18):
         for _ in range(2):
             t0 = time.perf_counter()
             encode_host_batch(schema, hc, chunk_blobs=chunk, want_status=False, out=out, offsets=offs)
@@ -233,8 +268,14 @@ def host_leg(schema, hc):
                 best = (el, chunk)
     el, chunk = best
     tot = int(offs[hc.n])
+    b_in = hc.nbytes_in()
+    b_out = tot + (0 if schema.fixed_blob_size > 0 else 8 * hc.n)   # arena + blob offsets
+    ideal = max(b_in / (pcie["bidir_each_gbs"] * 1e9), b_out / (pcie["bidir_each_gbs"] * 1e9),
+                b_in / (pcie["h2d_gbs"] * 1e9), b_out / (pcie["d2h_gbs"] * 1e9))
     enc = {"million_blobs_per_s": round(hc.n / el / 1e6, 3), "gib_per_s_out": round(tot / el / 2 ** 30, 3),
-           "gib_per_s_in_plus_out": round((tot + hc.nbytes_in()) / el / 2 ** 30, 3),
+           "gib_per_s_in_plus_out": round((tot + b_in) / el / 2 ** 30, 3),
+           "bytes_in": b_in, "bytes_out": b_out, "ms": round(el * 1e3, 3),
+           "frac_of_pcie": round(ideal / el, 3), "pcie": pcie,
            "chunk_blobs": chunk, "note": "pinned host columns -> packos_encode_host_batch -> pinned host arena"}
     # the read side: the pinned arena just produced -> packos_decode_host_batch
     # -> pinned host columns (views into the host arena)
@@ -247,7 +288,7 @@ def host_leg(schema, hc):
     hst = pinned(max(hc.n, 1), np.uint32)
     fixed = schema.fixed_blob_size > 0 and all(v is None for v in hc.valid)
     dbest = None
-    for chunk in (1 << 18, 1 << 20):
+    for chunk in (1 << 15, 1 << 16, 1 << 17, 1 << 18):
         for _ in range(2):
             t0 = time.perf_counter()
             if fixed:
@@ -259,8 +300,17 @@ def host_leg(schema, hc):
             if dbest is None or el < dbest[0]:
                 dbest = (el, chunk)
     ok = bool((hst[:hc.n] == 0).all())
+    d_out = 4 * hc.n
+    for sp in schema.specs:
+        d_out += hc.n * sp.width if sp.fixed else (12 * hc.n if sp.var else 0)
+        d_out += hc.n if sp.has_valid else 0
+    d_in = tot + (0 if fixed else 8 * (hc.n + 1))
+    dideal = max(d_in / (pcie["bidir_each_gbs"] * 1e9), d_out / (pcie["bidir_each_gbs"] * 1e9),
+                 d_in / (pcie["h2d_gbs"] * 1e9), d_out / (pcie["d2h_gbs"] * 1e9))
     enc["decode"] = {"million_blobs_per_s": round(hc.n / dbest[0] / 1e6, 3),
                      "gib_per_s_in": round(tot / dbest[0] / 2 ** 30, 3), "chunk_blobs": dbest[1], "all_ok": ok,
+                     "bytes_in": d_in, "bytes_out": d_out, "ms": round(dbest[0] * 1e3, 3),
+                     "frac_of_pcie": round(dideal / dbest[0], 3),
                      "note": "pinned host arena -> packos_decode_host_batch -> pinned host columns"}
     return enc
 
@@ -473,7 +523,7 @@ def main():
                   "checked": "every rank: its GPU shard vs the CPU oracle's encoding of the same global slice"}
     if rank == 0 and world == 1 and not args.no_host:
         try:
-            host = host_leg(schema, make_columns(cfg, n=min(n, 1 << 22), lo=lo))
+            host = host_leg(schema, make_columns(cfg, n=min(n, 1 << 22), lo=lo), dev)
         except Exception as e:  # reported, never fatal for the device-resident metric
             host = {"error": str(e)[:200]}
 

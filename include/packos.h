@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define PACKOS_ABI_VERSION 2
+#define PACKOS_ABI_VERSION 3
 
 /* ---- return codes (library-level errors) -------------------------------- */
 #define PACKOS_OK              0
@@ -298,13 +298,33 @@ int packos_encode_batch(const packos_schema* s, const packos_column* cols, size_
 
 /* ---- host-resident batches ------------------------------------------------ */
 
+/* A host pipeline: the device buffers, three HIP streams (H2D, kernels, D2H)
+ * and events of a chunked host <-> device loop, bound to the device current
+ * at creation and kept across calls (buffers grow on demand, never shrink),
+ * so a steady stream of host batches pays no allocation.  Chunk k's H2D runs
+ * while chunk k-1's kernels and chunk k-2's D2H run: both PCIe directions
+ * busy at once.  `slots` (>= 2; 0 = 3) chunks are in flight; chunk_blobs 0 =
+ * 131072.  One call at a time per pipeline (calls serialise on its lock);
+ * the schema must outlive it.  packos_encode_host_batch /
+ * packos_decode_host_batch use a pipeline cached on the schema handle.     */
+typedef struct packos_pipeline packos_pipeline;
+int  packos_pipeline_create(const packos_schema* s, size_t chunk_blobs, int slots, packos_pipeline** out);
+void packos_pipeline_free(packos_pipeline* p);
+/* packos_encode_host_batch / packos_decode_host_batch on an explicit
+ * pipeline (same arguments and results; chunking from the pipeline)        */
+int  packos_pipeline_encode(packos_pipeline* p, const packos_column* host_cols, size_t n_blobs, uint8_t* host_out,
+                            uint64_t out_capacity, uint64_t* host_offsets, uint32_t* host_status);
+int  packos_pipeline_decode(packos_pipeline* p, const uint8_t* host_arena, const uint64_t* host_offsets,
+                            uint64_t stride, size_t n_blobs, packos_column* host_cols, uint32_t* host_status);
+
 /* Encode n blobs whose columns live in HOST memory into a host arena — the
  * entry point a cgo / JNI shim calls for RPC payloads or BadgerDB values
  * (PackAppend / Pack per blob, access/put.go:619-681, for a whole batch).
- * Chunks of `chunk_blobs` blobs (0 = 1M) move through device buffers on two
- * streams of the current device: hipMemcpyAsync H2D, the size kernel + encode
- * kernel (or the fixed-layout kernel), D2H; one chunk's copies overlap the
- * other's kernels.  Pinned host buffers (hipHostMalloc / hipHostRegister)
+ * Chunks of `chunk_blobs` blobs (0 = 131072) move through the schema's
+ * cached pipeline on the current device (packos_pipeline_create): H2D of
+ * chunk k, the encode kernel(s) of chunk k-1 and D2H of chunk k-2 run at
+ * once.  Var columns go over as they are (data bytes + offsets of either
+ * width, no host rebasing).  Pinned host buffers (hipHostMalloc / hipHostRegister)
  * make the copies asynchronous; pageable ones work too.  host_cols use the
  * same layout as packos_encode_batch's device columns.  host_offsets (n+1)
  * receives the blob starts (required for variable-size batches); host_status
@@ -318,9 +338,10 @@ int packos_encode_host_batch(const packos_schema* s, const packos_column* host_c
  * cgo shim (BadgerDB values, RPC payloads: DecodeBuffer per blob,
  * schema/schema.go:893).  Blob i = host_arena[host_offsets[i] ..
  * host_offsets[i+1]) or, with host_offsets NULL, the `stride`-byte slot i.
- * Chunks of `chunk_blobs` blobs (0 = 1M) go H2D (their offsets and the arena
- * bytes they span), through packos_decode_batch, and D2H, on two streams of
- * the current device so one chunk's copies overlap the other's kernel.
+ * Chunks of `chunk_blobs` blobs (0 = 131072) go H2D (their offsets and the
+ * arena bytes between the chunk's smallest and largest offset), through
+ * packos_decode_batch, and D2H, pipelined like the encode side.  Offsets need
+ * not be monotone (a blob whose end precedes its start fails to decode).
  * host_cols use packos_decode_batch's layout in host memory; var views are
  * absolute host_arena offsets (or PACKOS_VIEW_DEFAULT); validity is written
  * for nullable leaves and containers; rows the decoder does not write (nil

@@ -27,7 +27,7 @@ from .columns import HostColumns, column_specs
 from .schema import SchemaChain
 
 __all__ = ["CompiledSchema", "DeviceColumns", "DecodedColumns", "HostDecoded", "encode_batch", "decode_batch",
-           "encode_host_batch", "decode_host_batch",
+           "encode_host_batch", "decode_host_batch", "Pipeline",
            "get_field_batch", "get_batch", "get_map_batch", "GET_FIXED", "GET_NULLABLE", "GET_SPAN", "GET_INT",
            "GET_FLOAT", "GET_ANY", "GET_EXTENDED", "MAP_STR", "MAP_ANY", "MODE_PUTACCESS", "MODE_PACKABLE", "MODE_EXTENDED"]
 
@@ -242,14 +242,10 @@ def host_batch_bound(schema: CompiledSchema, hc: HostColumns) -> int:
     return max(16, hc.n * max(stat, 0) + var_bytes)
 
 
-def encode_host_batch(schema: CompiledSchema, hc: HostColumns, chunk_blobs: int = 0,
-                      want_status: bool = True, out=None, offsets=None, status=None):
-    """Host-resident batch -> host arena through packos_encode_host_batch
-    (chunked H2D / encode / D2H on two streams of the current device; the
-    entry point a cgo shim binds).  `out` / `offsets` / `status` may be
-    preallocated numpy arrays (e.g. views of pinned memory).  Returns
-    (arena, offsets, status); arena is trimmed to the encoded bytes."""
-    L = lib()
+def _host_encode_args(schema: CompiledSchema, hc: HostColumns, want_status, out, offsets, status):
+    """ctypes column array (+ the arrays it points into) and the output
+    buffers of a host-resident encode.  A uint64 offsets array binds as
+    offsets64 (arenas past 4 GiB)."""
     n = hc.n
     keep = []
     arr = (PackosColumn * max(1, len(schema.specs)))()
@@ -260,18 +256,77 @@ def encode_host_batch(schema: CompiledSchema, hc: HostColumns, chunk_blobs: int 
                 continue
             a = np.ascontiguousarray(a)
             keep.append(a)
+            if name == "offsets" and a.dtype == np.uint64:
+                name = "offsets64"
             setattr(arr[c], name, a.ctypes.data)
     if out is None:
         out = np.empty(host_batch_bound(schema, hc), dtype=np.uint8)
-    cap = out.size
     offs = offsets if offsets is not None else np.empty(n + 1, dtype=np.uint64)
     want_status = want_status or schema.has_checks
     st = status if status is not None else (np.empty(max(n, 1), dtype=np.uint32) if want_status else None)
-    check(L.packos_encode_host_batch(schema.handle, arr, n, out.ctypes.data, cap, offs.ctypes.data,
-                                     None if st is None else st.ctypes.data, chunk_blobs),
+    return arr, keep, out, offs, st
+
+
+def encode_host_batch(schema: CompiledSchema, hc: HostColumns, chunk_blobs: int = 0,
+                      want_status: bool = True, out=None, offsets=None, status=None):
+    """Host-resident batch -> host arena through packos_encode_host_batch
+    (the schema's cached pipeline on the current device: H2D, kernels and D2H
+    of consecutive chunks overlap; the entry point a cgo shim binds).  `out` /
+    `offsets` / `status` may be preallocated numpy arrays (e.g. views of
+    pinned memory).  Returns (arena, offsets, status); arena is trimmed to the
+    encoded bytes."""
+    n = hc.n
+    arr, keep, out, offs, st = _host_encode_args(schema, hc, want_status, out, offsets, status)
+    check(lib().packos_encode_host_batch(schema.handle, arr, n, out.ctypes.data, out.size, offs.ctypes.data,
+                                         None if st is None else st.ctypes.data, chunk_blobs),
           "packos_encode_host_batch")
     del keep
     return out[: int(offs[n])], offs, (st[:n] if st is not None else None)
+
+
+class Pipeline:
+    """An explicit host pipeline (packos_pipeline_create): device buffers,
+    streams and events kept across calls, bound to the current device.  The
+    schema must outlive it."""
+
+    def __init__(self, schema: CompiledSchema, chunk_blobs: int = 0, slots: int = 0):
+        self.schema = schema
+        h = C.c_void_p()
+        check(lib().packos_pipeline_create(schema.handle, chunk_blobs, slots, C.byref(h)), "packos_pipeline_create")
+        self._h = h
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib().packos_pipeline_free(h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def encode(self, hc: HostColumns, want_status: bool = True, out=None, offsets=None, status=None):
+        """packos_pipeline_encode: (arena, offsets, status) like encode_host_batch."""
+        n = hc.n
+        arr, keep, out, offs, st = _host_encode_args(self.schema, hc, want_status, out, offsets, status)
+        check(lib().packos_pipeline_encode(self._h, arr, n, out.ctypes.data, out.size, offs.ctypes.data,
+                                           None if st is None else st.ctypes.data), "packos_pipeline_encode")
+        del keep
+        return out[: int(offs[n])], offs, (st[:n] if st is not None else None)
+
+    def decode(self, arena: np.ndarray, offsets: Optional[np.ndarray], n: int, stride: int = 0,
+               out: Optional["HostDecoded"] = None, status: Optional[np.ndarray] = None):
+        """packos_pipeline_decode: (HostDecoded, status) like decode_host_batch."""
+        a = np.ascontiguousarray(arena, dtype=np.uint8)
+        o = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+        out = out if out is not None else HostDecoded(self.schema, n)
+        st = status if status is not None else np.empty(max(n, 1), np.uint32)
+        check(lib().packos_pipeline_decode(self._h, a.ctypes.data if a.size else None,
+                                           None if o is None else o.ctypes.data, stride, n, out.ctypes_array(),
+                                           st.ctypes.data), "packos_pipeline_decode")
+        return out, st[:n]
 
 
 class HostDecoded:
@@ -302,8 +357,8 @@ def decode_host_batch(schema: CompiledSchema, arena: np.ndarray, offsets: Option
                       stride: int = 0, chunk_blobs: int = 0, out: Optional[HostDecoded] = None,
                       status: Optional[np.ndarray] = None):
     """DecodeBuffer over a HOST-resident batch through packos_decode_host_batch
-    (chunked H2D / decode / D2H on two streams; the cgo shim's read entry
-    point).  Returns (HostDecoded, status)."""
+    (the schema's cached pipeline: chunked H2D / decode / D2H overlapped; the
+    cgo shim's read entry point).  Returns (HostDecoded, status)."""
     a = np.ascontiguousarray(arena, dtype=np.uint8)
     o = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
     out = out if out is not None else HostDecoded(schema, n)

@@ -359,6 +359,15 @@ __global__ void k_fill_offsets(uint64_t* offs, uint64_t n, uint64_t B) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i <= n) offs[i] = i * B;
 }
+// host pipelines: offs[i] = base + i * B for i <= n; or offs[i] += add for i < n
+__global__ void k_fill_offsets_base(uint64_t* offs, uint64_t n, uint64_t base, uint64_t B) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= n) offs[i] = base + i * B;
+}
+__global__ void k_add_base(uint64_t* offs, uint64_t n, uint64_t add) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) offs[i] += add;
+}
 
 // =========================================================================
 // variable-size encode
@@ -1702,10 +1711,27 @@ int packos::upload_tables(packos_schema* s, int device, DeviceTables** out) {
     return PACKOS_OK;
 }
 
+namespace packos {
+int launch_fill_offsets(uint64_t* offs, size_t n, uint64_t base, uint64_t B, hipStream_t st) {
+    hipLaunchKernelGGL(k_fill_offsets_base, dim3((unsigned)((n + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, offs,
+                       (uint64_t)n, base, B);
+    HIP_TRY(hipGetLastError());
+    return PACKOS_OK;
+}
+int launch_add_base(uint64_t* offs, size_t n, uint64_t add, hipStream_t st) {
+    if (n == 0 || add == 0) return PACKOS_OK;
+    hipLaunchKernelGGL(k_add_base, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, offs, (uint64_t)n,
+                       add);
+    HIP_TRY(hipGetLastError());
+    return PACKOS_OK;
+}
+}  // namespace packos
+
 extern "C" {
 
 void packos_schema_free(packos_schema* s) {
     if (!s) return;
+    packos::destroy_pipelines(s);
     for (auto& d : s->dev) {
         if (d.block) {
             int cur = -1;

@@ -1,5 +1,7 @@
 // schema_impl.h — host representation of a compiled schema (packos_schema).
 #pragma once
+#include <hip/hip_runtime_api.h>
+
 #include <deque>
 #include <mutex>
 #include <string>
@@ -108,6 +110,9 @@ struct packos_schema {
 
     std::mutex mu;
     std::deque<packos::DeviceTables> dev;   // deque: pointers handed out stay valid
+    // host-resident batches: one cached pipeline per device (host_pipeline.cpp),
+    // created on first use by packos_encode_host_batch / packos_decode_host_batch
+    std::vector<packos_pipeline*> pipes;
 };
 
 namespace packos {
@@ -123,4 +128,9 @@ bool canonical_decodes(const packos_schema* s);
 uint64_t ext_layout_host(const packos_schema* s, std::vector<int64_t>& sz);
 // extended mode: bytes every container's extended header block may add to a blob
 int64_t ext_overhead(const packos_schema* s);
+// host pipelines (host_pipeline.cpp): free the schema's cached pipelines
+void destroy_pipelines(packos_schema* s);
+// tiny device helpers (kernels.hip) for the host pipelines
+int launch_fill_offsets(uint64_t* offs, size_t n, uint64_t base, uint64_t B, hipStream_t st);
+int launch_add_base(uint64_t* offs, size_t n, uint64_t add, hipStream_t st);
 }  // namespace packos

@@ -1053,6 +1053,58 @@ def test_decode_host_batch(name, n, chunk, pinned):
         _same_host_decode(cfg.chain, arena, None, n, got, st, name + " stride", stride=B)
 
 
+def test_pipeline_reuse_across_calls():
+    """One explicit packos_pipeline for many calls: more chunks than slots,
+    batches that grow (buffers reallocated) and shrink (reused), pinned and
+    pageable inputs, 32- and 64-bit host var offsets whose first value is not
+    0, then decode of each result on the same pipeline, all vs the oracle."""
+    from packos_amd.api import Pipeline
+    T = torch()
+    cfg = CONFIGS["C3"]
+    s = CompiledSchema(cfg.chain, cfg.mode)
+    p = Pipeline(s, chunk_blobs=1000, slots=3)
+    for n, lo, pinned, w64 in ((5000, 0, False, False), (23456, 777, True, False), (1500, 5, False, True),
+                               (9000, 123457, True, True)):
+        hc = make_columns(cfg, n=n, lo=lo)
+        a0, o0, s0 = ob.encode(cfg.chain, hc, cfg.mode, nthreads=8)
+        for c, o in enumerate(hc.offsets):
+            if o is not None:   # offsets into a bigger host arena: values start past 0
+                shift = 4096 + 3 * c
+                hc.data[c] = np.concatenate([np.full(shift, 0xAB, np.uint8), hc.data[c]])
+                hc.offsets[c] = (o.astype(np.uint64) + shift).astype(np.uint64 if w64 else np.uint32)
+        if pinned:
+            for lst in (hc.data, hc.offsets):
+                for c, a in enumerate(lst):
+                    if a is not None:
+                        lst[c] = T.from_numpy(np.ascontiguousarray(a).view(np.int64 if a.dtype == np.uint64 else a.dtype)
+                                              ).pin_memory().numpy().view(a.dtype)
+        a1, o1, s1 = p.encode(hc)
+        assert np.array_equal(o0, o1) and np.array_equal(a0, a1) and np.array_equal(s0, s1.astype(np.uint32)), n
+        got, st = p.decode(a1, o1, n)
+        _same_host_decode(cfg.chain, a1, o1, n, got, st, f"pipeline n={n}")
+    p.close()
+
+
+def test_decode_host_batch_nonmonotone_offsets():
+    """Offsets that go backwards inside a chunk: the chunk's staged range is
+    [min, max) of its offsets, so every blob reads staged bytes; a blob whose
+    end precedes its start fails like the oracle's."""
+    from packos_amd.api import decode_host_batch
+    cfg = CONFIGS["C3"]
+    n = 4000
+    hc = make_columns(cfg, n=n)
+    arena, offs, _ = ob.encode(cfg.chain, hc, cfg.mode, nthreads=8)
+    offs = offs.copy()
+    rng = np.random.default_rng(5)
+    for i in rng.integers(1, n - 1, size=40):   # swap a blob boundary with its neighbour's
+        offs[i], offs[i + 1] = offs[i + 1], offs[i]
+    offs[1000] = offs[3500]                     # a jump forward, then back
+    s = CompiledSchema(cfg.chain, cfg.mode)
+    got, st = decode_host_batch(s, arena, offs, n, chunk_blobs=512)
+    _same_host_decode(cfg.chain, arena, offs, n, got, st, "nonmonotone")
+    assert (st != 0).any() and (st == 0).any()
+
+
 @pytest.mark.parametrize("seed", range(0, 40, 4))
 def test_decode_host_batch_random(seed):
     """Random schemas, checked schemas and corrupted blobs; offsets that start

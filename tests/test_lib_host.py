@@ -28,7 +28,7 @@ def test_exports_match_header():
     for name in sorted(declared):
         assert hasattr(L, name), f"{name} declared in packos.h but not exported"
     assert set(_lib.EXPORTED) == declared
-    assert L.packos_abi_version() == 2
+    assert L.packos_abi_version() == 3
 
 
 def test_schema_errors():
