@@ -1300,12 +1300,35 @@ struct PathArg {
 
 // One thread per blob: walk the nested path (GetNestedGetAccess, get.go:377-
 // 401), then apply one Get* family (see packos_get_batch in packos.h) and
-// optionally gather the typed value into a dense output row.
+// optionally gather the typed value into a dense output row.  Every output
+// is written exactly once, at the end (a value of <= 8 bytes as one store).
+__device__ __forceinline__ uint64_t gwin_le(const GWin& r, uint64_t at, int64_t w) {
+    const uint64_t d = at - r.base;
+    if (d + 8 <= r.n) {   // inside the register window: funnel-shift three words
+        const uint32_t k = (uint32_t)d >> 2, q = (uint32_t)d & 3u;
+        uint32_t w0 = 0, w1 = 0, w2 = 0;
+#pragma unroll
+        for (uint32_t x = 0; x < kGetWin / 4; x++) {
+            w0 = x == k ? r.W[x] : w0;
+            w1 = x == k + 1 ? r.W[x] : w1;
+            w2 = x == k + 2 ? r.W[x] : w2;
+        }
+        const uint32_t lo = q ? __builtin_amdgcn_alignbyte(w1, w0, q) : w0;
+        const uint32_t hi = q ? __builtin_amdgcn_alignbyte(w2, w1, q) : w1;
+        uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
+        return w >= 8 ? v : v & ((1ull << (8 * w)) - 1);
+    }
+    uint64_t v = 0;
+    for (int64_t k = 0; k < w && k < 8; k++) v |= (uint64_t)r.byte(at + k) << (8 * k);
+    return v;
+}
+
 __global__ __launch_bounds__(kBlock) void k_get_field(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                                                       uint64_t stride, uint64_t n, PathArg path, int depth, int getter,
                                                       int want_tag, int want_width, uint8_t* __restrict__ out_values,
-                                                      uint32_t value_width, uint64_t* out_start, uint32_t* out_len,
-                                                      uint8_t* out_tag, uint8_t* status) {
+                                                      uint32_t value_width, uint64_t* __restrict__ out_start,
+                                                      uint32_t* __restrict__ out_len, uint8_t* __restrict__ out_tag,
+                                                      uint8_t* __restrict__ status) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t a0 = offs ? offs[i] : i * stride;
@@ -1322,67 +1345,86 @@ __global__ __launch_bounds__(kBlock) void k_get_field(const uint8_t* __restrict_
         r.W[0] = w0.x; r.W[1] = w0.y; r.W[2] = w0.z; r.W[3] = w0.w;
         r.W[4] = w1.x; r.W[5] = w1.y; r.W[6] = w1.z; r.W[7] = w1.w;
     }
-    out_start[i] = 0; out_len[i] = 0; out_tag[i] = 0;
-    uint8_t* dst = out_values ? out_values + i * value_width : nullptr;
-    if (dst)
-        for (uint32_t k = 0; k < value_width; k++) dst[k] = 0;
     const bool xmode = (getter & PACKOS_GET_EXTENDED) != 0;
     getter &= ~PACKOS_GET_EXTENDED;
+    uint64_t o_start = 0, val = 0;
+    uint32_t o_len = 0;
+    int o_tag = 0, rc = 0;
+    int64_t w = 0, s = 0, e = 0;
+    bool big = false;   // a FIXED / NULLABLE value wider than 8 bytes (byte copy below)
     DGet g;
     const bool xtop = xmode && a1 - a0 >= 2 && r.u16(a0) == kExtMarker;
     if (!(xtop ? dget_init_ext(g, r, a0, (int64_t)(a1 - a0), true) : dget_init(g, r, a0, (int64_t)(a1 - a0)))) {
-        status[i] = 3;
-        return;
-    }
-    int tp; int64_t s, e;
-    for (int d = 0; d < depth - 1; d++) {
-        dget_range(g, r, path.p[d], tp, s, e);
-        const bool x = xmode && tp == PACKOS_TAG_EXTENDED;
-        if (e < s || (tp != 7 && tp != 4 && !x)) { status[i] = 1; return; }
-        if (e == s) { status[i] = 2; return; }
-        DGet nx;
-        if (x) {
-            if (!dget_init_ext(nx, r, g.start + (uint64_t)s, e - s, false)) { status[i] = 1; return; }
-        } else if (!dget_init(nx, r, g.start + (uint64_t)s, e - s)) {
-            status[i] = 3;
-            return;
-        }
-        g = nx;
-    }
-    dget_range(g, r, path.p[depth - 1], tp, s, e);
-    out_tag[i] = (uint8_t)tp;
-    const int64_t w = e - s;
-    int rc = 0;
-    switch (getter) {
-        case PACKOS_GET_NULLABLE:
-            if (w == 0) { rc = 4; break; }
-            [[fallthrough]];
-        case PACKOS_GET_FIXED: rc = (tp != want_tag || w != want_width); break;
-        case PACKOS_GET_SPAN: rc = (tp != want_tag || e < s); break;
-        case PACKOS_GET_INT:
-            rc = tp != PACKOS_TAG_INTEGER ? 1 : w == 0 ? 4 : (w != 1 && w != 2 && w != 4 && w != 8);
-            break;
-        case PACKOS_GET_FLOAT: rc = tp != PACKOS_TAG_FLOATING ? 1 : w == 0 ? 4 : (w != 4 && w != 8); break;
-        case PACKOS_GET_ANY:   // GetTypeAndValue (get.go:504-510); past argCount buf[-2:-1] panics
-            rc = s < 0 ? 3 : e < s ? 1 : 0;
-            break;
-        default: rc = 1;
-    }
-    status[i] = (uint8_t)rc;
-    if (rc) return;
-    const uint64_t at = g.start + (uint64_t)s;
-    out_start[i] = at;
-    out_len[i] = (uint32_t)w;
-    if (!dst || getter == PACKOS_GET_SPAN || getter == PACKOS_GET_ANY) return;
-    if (getter == PACKOS_GET_INT) {
-        uint64_t v = 0;
-        for (int k = 0; k < w; k++) v |= (uint64_t)r.byte(at + k) << (8 * k);
-        if (w < 8 && ((v >> (8 * w - 1)) & 1)) v |= ~0ull << (8 * w);
-        for (uint32_t k = 0; k < 8 && k < value_width; k++) dst[k] = (uint8_t)(v >> (8 * k));
-    } else if (tp == PACKOS_TAG_BOOL && w == 1) {
-        dst[0] = r.byte(at) != 0;
+        rc = 3;
     } else {
-        for (int64_t k = 0; k < w && k < (int64_t)value_width; k++) dst[k] = (uint8_t)r.byte(at + k);
+        int tp;
+        for (int d = 0; d < depth - 1 && !rc; d++) {
+            dget_range(g, r, path.p[d], tp, s, e);
+            const bool x = xmode && tp == PACKOS_TAG_EXTENDED;
+            if (e < s || (tp != 7 && tp != 4 && !x)) { rc = 1; break; }
+            if (e == s) { rc = 2; break; }
+            DGet nx;
+            if (x) {
+                if (!dget_init_ext(nx, r, g.start + (uint64_t)s, e - s, false)) { rc = 1; break; }
+            } else if (!dget_init(nx, r, g.start + (uint64_t)s, e - s)) {
+                rc = 3;
+                break;
+            }
+            g = nx;
+        }
+        if (!rc) {
+            dget_range(g, r, path.p[depth - 1], tp, s, e);
+            o_tag = tp;
+            w = e - s;
+            switch (getter) {
+                case PACKOS_GET_NULLABLE:
+                    if (w == 0) { rc = 4; break; }
+                    [[fallthrough]];
+                case PACKOS_GET_FIXED: rc = (tp != want_tag || w != want_width); break;
+                case PACKOS_GET_SPAN: rc = (tp != want_tag || e < s); break;
+                case PACKOS_GET_INT:
+                    rc = tp != PACKOS_TAG_INTEGER ? 1 : w == 0 ? 4 : (w != 1 && w != 2 && w != 4 && w != 8);
+                    break;
+                case PACKOS_GET_FLOAT: rc = tp != PACKOS_TAG_FLOATING ? 1 : w == 0 ? 4 : (w != 4 && w != 8); break;
+                case PACKOS_GET_ANY:   // GetTypeAndValue (get.go:504-510); past argCount buf[-2:-1] panics
+                    rc = s < 0 ? 3 : e < s ? 1 : 0;
+                    break;
+                default: rc = 1;
+            }
+            if (!rc) {
+                const uint64_t at = g.start + (uint64_t)s;
+                o_start = at;
+                o_len = (uint32_t)w;
+                if (out_values && getter != PACKOS_GET_SPAN && getter != PACKOS_GET_ANY) {
+                    if (getter == PACKOS_GET_INT) {
+                        val = gwin_le(r, at, w);
+                        if (w < 8 && ((val >> (8 * w - 1)) & 1)) val |= ~0ull << (8 * w);   // sign-extend
+                    } else if (tp == PACKOS_TAG_BOOL && w == 1) {
+                        val = gwin_le(r, at, 1) != 0;
+                    } else if (w <= 8) {
+                        val = gwin_le(r, at, w);
+                    } else {
+                        big = true;
+                    }
+                }
+            }
+        }
+    }
+    out_start[i] = o_start;
+    out_len[i] = o_len;
+    out_tag[i] = (uint8_t)o_tag;
+    status[i] = (uint8_t)rc;
+    if (!out_values) return;
+    uint8_t* dst = out_values + i * value_width;
+    if (value_width == 8 && ((uintptr_t)dst & 7) == 0) {
+        *(uint64_t*)dst = val;
+    } else if (value_width == 4 && ((uintptr_t)dst & 3) == 0) {
+        *(uint32_t*)dst = (uint32_t)val;
+    } else if (!big) {
+        for (uint32_t k = 0; k < value_width; k++) dst[k] = k < 8 ? (uint8_t)(val >> (8 * k)) : 0;
+    } else {
+        const uint64_t at = o_start;
+        for (uint32_t k = 0; k < value_width; k++) dst[k] = k < (uint64_t)w ? (uint8_t)r.byte(at + k) : 0;
     }
 }
 

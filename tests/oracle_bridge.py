@@ -13,7 +13,8 @@ from typing import List, Optional
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+# PACKOS_ORACLE_LIB: the sanitizer build of tools/asan_cpu.sh (test runs only)
+ORACLE_SO = os.environ.get("PACKOS_ORACLE_LIB") or os.path.join(ROOT, "oracle", "liboracle.so")
 
 MODE_PUTACCESS = 0
 MODE_PACKABLE = 1
