@@ -637,6 +637,24 @@ struct WReader {
         return (*this)(p) | ((*this)(p + 1) << 8);
     }
 };
+// LDS-window reader without bounds checks or HBM fallback, for reads the
+// caller has proven to lie inside the window (dword k at win32[k * stride]).
+// Reads of 2 / 4 bytes are two dword reads + v_alignbyte, branch-free.
+struct LReader {
+    const uint32_t* win32;
+    uint64_t base;
+    uint32_t stride;
+    __device__ __forceinline__ uint32_t dw(uint32_t k) const { return win32[k * stride]; }
+    __device__ __forceinline__ uint32_t u32(uint64_t p) const {
+        const uint32_t d = (uint32_t)(p - base), k = d >> 2;
+        return __builtin_amdgcn_alignbyte(dw(k + 1), dw(k), d & 3u);
+    }
+    __device__ __forceinline__ uint32_t u16(uint64_t p) const { return u32(p) & 0xFFFFu; }
+    __device__ __forceinline__ uint32_t operator()(uint64_t p) const {
+        const uint32_t d = (uint32_t)(p - base);
+        return (dw(d >> 2) >> (8 * (d & 3u))) & 0xFFu;
+    }
+};
 template <class R>
 __host__ __device__ __forceinline__ uint16_t rd16r(const R& r, uint64_t p) { return (uint16_t)r.u16(p); }
 
@@ -966,6 +984,85 @@ __device__ __forceinline__ uint32_t decode_flat(const DecProgram& P, const DecCo
     return 0;
 }
 
+// Flat chains of plain leaves (no value checks / literals / defaults, plain
+// modes): the canonical fast path with each field's descriptor packed into
+// one word and its output pointers resolved on the host, all passed by value:
+// every per-field value is a uniform kernel-argument (scalar) load, so the
+// field loop is scalar control around a few vector ops per blob instead of a
+// node-table walk.  Pass 1 validates exactly what decode_flat does (tags,
+// monotone offsets, fixed widths / nil nullables, End = len); pass 2 re-reads
+// the header words (LDS) and writes each field with one store of its width.
+// A blob that is not canonical returns kFlatFallback.
+constexpr int kFlatMax = 16;
+struct FlatArg {
+    int32_t F;                 // 0: not eligible (decode_flat / decode_blob decide)
+    uint32_t fd[kFlatMax];     // kind | width << 4 | tag << 20 | nullable << 23
+    uint64_t p0[kFlatMax];     // fixed: row base (n x width); var: view starts
+    uint64_t p1[kFlatMax];     // nullable fixed: validity; var: view lengths
+};
+__device__ __forceinline__ int fd_kind(uint32_t d) { return (int)(d & 15u); }
+__device__ __forceinline__ int fd_width(uint32_t d) { return (int)(int16_t)((d >> 4) & 0xFFFFu); }   // <= 0: var
+__device__ __forceinline__ int fd_tag(uint32_t d) { return (int)((d >> 20) & 7u); }
+__device__ __forceinline__ bool fd_null(uint32_t d) { return (d >> 23) & 1u; }
+
+template <class R>
+__device__ __forceinline__ uint32_t decode_flat_k(const FlatArg& A, const R& r, uint64_t a0, uint64_t a1, uint64_t i) {
+    const int F = A.F;
+    const int64_t len = (int64_t)(a1 - a0);
+    if (len < 2 * (F + 1)) return kFlatFallback;
+    const uint32_t h0 = r.u16(a0);
+    const int64_t base = h0 >> 3;
+    bool bad = base != 2 * (F + 1);
+    int64_t o = base;
+    uint32_t hj = h0;
+    for (int j = 0; j < F; j++) {
+        const uint32_t d = A.fd[j];
+        const uint32_t hn = r.u16(a0 + 2 * (j + 1));
+        const int64_t nx = (int64_t)(hn >> 3) + base;
+        const int64_t w = nx - o;
+        const int k = fd_kind(d), fw = fd_width(d);
+        bad |= (int)(hj & 7u) != fd_tag(d) || nx < o;
+        if (k == K_STRING || k == K_BYTES) bad |= fw > 0 && w != fw;
+        else bad |= w != fw && !(fd_null(d) && w == 0);
+        o = nx;
+        hj = hn;   // after the last field: the End header
+    }
+    // the End header: tag 0 and End offset == len
+    bad |= (hj & 7u) != 0 || o != len;
+    if (bad) return kFlatFallback;
+    o = base;
+    for (int j = 0; j < F; j++) {
+        const uint32_t d = A.fd[j];
+        const int64_t nx = (int64_t)(r.u16(a0 + 2 * (j + 1)) >> 3) + base;
+        const uint64_t pay = a0 + (uint64_t)o;
+        const uint32_t w = (uint32_t)(nx - o);
+        o = nx;
+        const int k = fd_kind(d), fw = fd_width(d);
+        // global (not flat) stores: the pointers are device memory
+        typedef __attribute__((address_space(1))) uint8_t g8;
+        typedef __attribute__((address_space(1))) uint16_t g16;
+        typedef __attribute__((address_space(1))) uint32_t g32;
+        typedef __attribute__((address_space(1))) uint64_t g64;
+        if ((k == K_STRING || k == K_BYTES) && fw <= 0) {
+            ((g64*)A.p0[j])[i] = w == 0 ? 0ull : pay;
+            ((g32*)A.p1[j])[i] = w;
+            continue;
+        }
+        if (fd_null(d) && A.p1[j]) ((g8*)A.p1[j])[i] = w != 0;
+        if (w == 0) continue;
+        g8* dp = (g8*)A.p0[j] + i * (uint64_t)fw;
+        if (fw == 1) *dp = k == K_BOOL ? (uint8_t)(r(pay) != 0) : (uint8_t)r(pay);
+        else if (fw == 2) *(g16*)dp = (uint16_t)r.u16(pay);
+        else if (fw == 4) *(g32*)dp = r.u32(pay);
+        else if (fw == 8) *(g64*)dp = (uint64_t)r.u32(pay) | ((uint64_t)r.u32(pay + 4) << 32);
+        else if ((fw & 3) == 0)
+            for (int x = 0; x < fw; x += 4) *(g32*)(dp + x) = r.u32(pay + x);
+        else
+            for (int x = 0; x < fw; x++) dp[x] = (uint8_t)r(pay + x);
+    }
+    return 0;
+}
+
 // Generic decode with a per-blob LDS window: every thread first fetches its
 // blob's first kDecWinChunks x 16 bytes (header block, leading fields) with
 // 16-B loads, all in flight, then runs decode_blob reading the window and
@@ -976,7 +1073,8 @@ constexpr int kDecWinChunks = 8;
 // WC: window chunks per blob — enough for the schema's static prefix (bytes
 // before the first var payload; compile.cpp), at most kDecWinChunks.
 template <int WC, bool EXT>
-__global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols cols, const uint8_t* __restrict__ arena,
+__global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols cols, FlatArg FA,
+                                                       const uint8_t* __restrict__ arena,
                                                        const uint64_t* __restrict__ offs, uint64_t stride, uint64_t n,
                                                        uint32_t* __restrict__ status) {
     __shared__ __attribute__((aligned(16))) uint8_t win[kBlock * kDecWinChunks * 16];
@@ -1046,7 +1144,17 @@ __global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols col
     const WReader R{arena, (const uint32_t*)w, b0, wbytes, tile_mode ? 1u : (uint32_t)kBlock};
     const DecProgram LP{lnodes, lkids, llits, P.root, P.n_nodes, P.n_kids, P.n_lits, P.flat, P.ext, P.win};
     uint32_t sv = kFlatFallback;
-    if (P.flat) sv = decode_flat(LP, cols, R, a0, a1, i);
+    if (FA.F) {
+        // the flat path reads only the header block and fixed payloads: inside
+        // the window when the tile holds the whole blob, or (per-blob windows)
+        // when no fixed payload follows a var one (P.win > 0: the window is the
+        // static prefix, which pass 1 confines every fixed payload to)
+        const bool inside = tile_mode ? (a0 >= b0 && a1 <= b0 + wbytes && a1 >= a0) : P.win > 0;
+        if (inside) sv = decode_flat_k(FA, LReader{(const uint32_t*)w, b0, tile_mode ? 1u : (uint32_t)kBlock}, a0, a1, i);
+        else sv = decode_flat_k(FA, R, a0, a1, i);
+    } else if (P.flat) {
+        sv = decode_flat(LP, cols, R, a0, a1, i);
+    }
     if (sv == kFlatFallback) sv = decode_blob<WReader, EXT>(LP, cols, R, a0, a1, i);
     status[i] = sv;
 }
@@ -2155,8 +2263,32 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
         // per-blob window: the static prefix from a 16-B aligned start (+15 B)
         const int64_t need = (s->dec_prefix + 15 + 15) / 16;
         const dim3 g((unsigned)((n + kBlock - 1) / kBlock));
-#define PACKOS_DECWIN(WC, X)                                                                             \
-    hipLaunchKernelGGL((k_decode_win<WC, X>), g, dim3(kBlock), ptab, st, t->dec, dc, arena, offsets, stride, \
+        // flat chains of plain leaves: field descriptors + output pointers by value
+        FlatArg FA;
+        memset(&FA, 0, sizeof(FA));
+        {
+            const Node& root = s->nodes[0];
+            bool ok = !s->ext && !s->tune.decode_generic && !root.kids.empty() && root.kids.size() <= (size_t)kFlatMax;
+            for (size_t j = 0; ok && j < root.kids.size(); j++) {
+                const Node& nd = s->nodes[root.kids[j]];
+                const DecNode& dn = s->dnodes[root.kids[j]];
+                ok = nd.kind >= K_INT && nd.kind <= K_BYTES && nd.check == 0 && dn.width < 0x8000;
+                if (!ok) break;
+                const bool scalar = nd.kind >= K_INT && nd.kind <= K_BOOL;
+                const bool var = !scalar && dn.width <= 0;
+                FA.fd[j] = (uint32_t)nd.kind | ((uint32_t)(dn.width & 0xFFFF) << 4) | ((uint32_t)dn.tag << 20) |
+                           ((dn.nullable ? 1u : 0u) << 23);
+                FA.p0[j] = (uint64_t)(uintptr_t)(var ? (void*)dc.start[nd.col] : (void*)dc.data[nd.col]);
+                FA.p1[j] = (uint64_t)(uintptr_t)(var ? (void*)dc.length[nd.col] : (void*)dc.valid[nd.col]);
+                if (scalar && (dn.width != 1 && dn.width != 2 && dn.width != 4 && dn.width != 8)) ok = false;
+                // one naturally aligned store per row (a 16-B aligned column base)
+                if (!var && (FA.p0[j] & 15)) ok = false;
+                if (var && ((FA.p0[j] & 7) || (FA.p1[j] & 3))) ok = false;
+            }
+            FA.F = ok ? (int32_t)root.kids.size() : 0;
+        }
+#define PACKOS_DECWIN(WC, X)                                                                                 \
+    hipLaunchKernelGGL((k_decode_win<WC, X>), g, dim3(kBlock), ptab, st, t->dec, dc, FA, arena, offsets, stride, \
                        (uint64_t)n, status)
         if (s->ext) {   // extended containers: bigger blobs, no window sizing games
             PACKOS_DECWIN(kDecWinChunks, true);
