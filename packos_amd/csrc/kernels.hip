@@ -1077,7 +1077,9 @@ __global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols col
                                                        const uint8_t* __restrict__ arena,
                                                        const uint64_t* __restrict__ offs, uint64_t stride, uint64_t n,
                                                        uint32_t* __restrict__ status) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[kBlock * kDecWinChunks * 16];
+    // sized by WC: the per-blob windows need kBlock * WC chunks, and a tile
+    // staged whole must fit the same bytes (LDS per workgroup sets occupancy)
+    __shared__ __attribute__((aligned(16))) uint8_t win[kBlock * WC * 16];
     extern __shared__ __attribute__((aligned(16))) uint8_t ptab[];   // decode program copy (nodes | kids | lits)
     const int tid = threadIdx.x;
     // the program is read once per visited field: keep it in LDS
@@ -2261,7 +2263,10 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
         const size_t ptab = ((s->dnodes.size() * sizeof(DecNode) + 15) & ~(size_t)15) +
                             ((s->dkids.size() * 4 + 15) & ~(size_t)15) + s->lits.size() + 16;
         // per-blob window: the static prefix from a 16-B aligned start (+15 B)
-        const int64_t need = (s->dec_prefix + 15 + 15) / 16;
+        // (a fixed payload after a var one is read past the prefix: keep >= 24 KB
+        // so tiles of such schemas stay staged whole)
+        int64_t need = (s->dec_prefix + 15 + 15) / 16;
+        if (s->dec_tail_fixed && need < 6) need = 6;
         const dim3 g((unsigned)((n + kBlock - 1) / kBlock));
         // flat chains of plain leaves: field descriptors + output pointers by value
         FlatArg FA;
@@ -2296,6 +2301,8 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
             PACKOS_DECWIN(2, false);
         } else if (need <= 4) {
             PACKOS_DECWIN(4, false);
+        } else if (need <= 6) {
+            PACKOS_DECWIN(6, false);
         } else {
             PACKOS_DECWIN(kDecWinChunks, false);
         }
