@@ -207,34 +207,66 @@ def shard_parity(cfg, hc, gpu_arena, gpu_offsets, threads):
     return same, hashlib.sha256(gpu_arena[:total].tobytes()).hexdigest()[:16]
 
 
-def pcie_ceiling(dev, nbytes=256 << 20, reps=5):
-    """Pinned host <-> device copy rates of this box (GB/s): H2D alone, D2H
-    alone, and both at once on two streams (the full-duplex ceiling a
-    pipelined host batch can reach)."""
+def pcie_ceiling(dev, nbytes=256 << 20, reps=4, piece=64 << 20):
+    """Pinned host <-> device copy rates of this box (GB/s) with plain HIP
+    calls (libamdhip64 through ctypes): H2D alone, D2H alone, and both at once
+    on two streams in `piece`-byte copies (the full-duplex ceiling a pipelined
+    host batch can reach; `bidir_total_gbs` = both directions' bytes / time)."""
+    import ctypes as C
     import torch
-    h_in = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
-    h_out = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
-    d_in = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    d_out = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    hip = C.CDLL("libamdhip64.so")
+    vp = C.c_void_p
+    hip.hipHostMalloc.argtypes = [C.POINTER(vp), C.c_size_t, C.c_uint]
+    hip.hipMalloc.argtypes = [C.POINTER(vp), C.c_size_t]
+    hip.hipMemcpyAsync.argtypes = [vp, vp, C.c_size_t, C.c_int, vp]
+    hip.hipStreamCreate.argtypes = [C.POINTER(vp)]
+    hip.hipStreamSynchronize.argtypes = [vp]
+    hip.hipFree.argtypes = [vp]
+    hip.hipHostFree.argtypes = [vp]
+    hip.hipStreamDestroy.argtypes = [vp]
+    h_in, h_out, d_in, d_out, s1, s2 = (vp() for _ in range(6))
+    ok = (hip.hipHostMalloc(C.byref(h_in), nbytes, 0) == 0 and hip.hipHostMalloc(C.byref(h_out), nbytes, 0) == 0 and
+          hip.hipMalloc(C.byref(d_in), nbytes) == 0 and hip.hipMalloc(C.byref(d_out), nbytes) == 0 and
+          hip.hipStreamCreate(C.byref(s1)) == 0 and hip.hipStreamCreate(C.byref(s2)) == 0)
+    if not ok:
+        return {"error": "HIP allocation failed"}
+    H2D, D2H = 1, 2
 
     def run(h2d, d2h):
-        torch.cuda.synchronize()
+        hip.hipStreamSynchronize(s1)
+        hip.hipStreamSynchronize(s2)
         t0 = time.perf_counter()
         for _ in range(reps):
-            if h2d:
-                with torch.cuda.stream(s1):
-                    d_in.copy_(h_in, non_blocking=True)
-            if d2h:
-                with torch.cuda.stream(s2):
-                    h_out.copy_(d_out, non_blocking=True)
-        torch.cuda.synchronize()
-        return nbytes * reps / (time.perf_counter() - t0) / 1e9
+            for off in range(0, nbytes, piece):
+                if h2d:
+                    hip.hipMemcpyAsync(vp(d_in.value + off), vp(h_in.value + off), piece, H2D, s1)
+                if d2h:
+                    hip.hipMemcpyAsync(vp(h_out.value + off), vp(d_out.value + off), piece, D2H, s2)
+        hip.hipStreamSynchronize(s1)
+        hip.hipStreamSynchronize(s2)
+        return nbytes * reps * (int(h2d) + int(d2h)) / (time.perf_counter() - t0) / 1e9
     run(True, True)
-    h2d, d2h = run(True, False), run(False, True)
-    both = run(True, True)
-    return {"h2d_gbs": round(h2d, 2), "d2h_gbs": round(d2h, 2), "bidir_each_gbs": round(both, 2),
-            "note": f"pinned torch copies of {nbytes >> 20} MiB x {reps}; bidir = H2D and D2H on two streams at once"}
+    h2d, d2h, both = run(True, False), run(False, True), run(True, True)
+    for p_ in (d_in, d_out):
+        hip.hipFree(p_)
+    for p_ in (h_in, h_out):
+        hip.hipHostFree(p_)
+    hip.hipStreamDestroy(s1)
+    hip.hipStreamDestroy(s2)
+    return {"h2d_gbs": round(h2d, 2), "d2h_gbs": round(d2h, 2), "bidir_total_gbs": round(both, 2),
+            "note": f"hipMemcpyAsync of pinned (hipHostMalloc) {nbytes >> 20} MiB x {reps} in {piece >> 20} MiB pieces; "
+                    "bidir = H2D and D2H on two streams at once, both directions' bytes / time"}
+
+
+def pcie_time(pcie, b_in, b_out):
+    """Seconds the box's PCIe needs for b_in bytes H2D and b_out bytes D2H
+    moving at once: each direction at most its one-way rate, both together at
+    most the measured bidirectional total."""
+    if "error" in pcie:
+        return float("nan")
+    return max(b_in / (pcie["h2d_gbs"] * 1e9), b_out / (pcie["d2h_gbs"] * 1e9),
+               (b_in + b_out) / (pcie["bidir_total_gbs"] * 1e9))
 
 
 def host_leg(schema, hc, dev):
@@ -270,8 +302,7 @@ def host_leg(schema, hc, dev):
     tot = int(offs[hc.n])
     b_in = hc.nbytes_in()
     b_out = tot + (0 if schema.fixed_blob_size > 0 else 8 * hc.n)   # arena + blob offsets
-    ideal = max(b_in / (pcie["bidir_each_gbs"] * 1e9), b_out / (pcie["bidir_each_gbs"] * 1e9),
-                b_in / (pcie["h2d_gbs"] * 1e9), b_out / (pcie["d2h_gbs"] * 1e9))
+    ideal = pcie_time(pcie, b_in, b_out)
     enc = {"million_blobs_per_s": round(hc.n / el / 1e6, 3), "gib_per_s_out": round(tot / el / 2 ** 30, 3),
            "gib_per_s_in_plus_out": round((tot + b_in) / el / 2 ** 30, 3),
            "bytes_in": b_in, "bytes_out": b_out, "ms": round(el * 1e3, 3),
@@ -305,8 +336,7 @@ def host_leg(schema, hc, dev):
         d_out += hc.n * sp.width if sp.fixed else (12 * hc.n if sp.var else 0)
         d_out += hc.n if sp.has_valid else 0
     d_in = tot + (0 if fixed else 8 * (hc.n + 1))
-    dideal = max(d_in / (pcie["bidir_each_gbs"] * 1e9), d_out / (pcie["bidir_each_gbs"] * 1e9),
-                 d_in / (pcie["h2d_gbs"] * 1e9), d_out / (pcie["d2h_gbs"] * 1e9))
+    dideal = pcie_time(pcie, d_in, d_out)
     enc["decode"] = {"million_blobs_per_s": round(hc.n / dbest[0] / 1e6, 3),
                      "gib_per_s_in": round(tot / dbest[0] / 2 ** 30, 3), "chunk_blobs": dbest[1], "all_ok": ok,
                      "bytes_in": d_in, "bytes_out": d_out, "ms": round(dbest[0] * 1e3, 3),
