@@ -188,10 +188,20 @@ def cpu_leg(cfg, hc, seconds, gpu_arena, gpu_offsets):
     return res, hi, same, digest, total
 
 
-def shard_parity(cfg, hc, gpu_arena, gpu_offsets, threads):
-    """One oracle encode of this rank's slice, compared with its GPU output."""
+def shard_parity(cfg, hc, gpu_arena, gpu_offsets, threads, max_blobs=1 << 21):
+    """One oracle encode of this rank's slice (its first `max_blobs` blobs
+    when the shard is larger: a C5 shard is 8 GB), compared with its GPU
+    output."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bridge as ob  # checker only
+    if hc.n > max_blobs:
+        from packos_amd.shard import slice_columns
+        m = max_blobs
+        if gpu_offsets is not None:
+            gpu_arena, gpu_offsets = gpu_arena[: int(gpu_offsets[m])], gpu_offsets[: m + 1]
+        else:   # fixed size: blob i at i * B
+            gpu_arena = gpu_arena[: m * (len(gpu_arena) // hc.n)]
+        hc = slice_columns(hc, 0, m)
     os_ = ob.OracleSchema(cfg.chain)
     keep = []
     cols = ob.make_cols(hc, keep)
@@ -549,8 +559,9 @@ def main():
         flag = torch.tensor([1 if same else 0], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         parity = {"result": "bit-exact" if int(flag.item()) == 1 else "MISMATCH", "ranks": world,
-                  "blobs_rank0": n, "sha256_16_rank0": digest,
-                  "checked": "every rank: its GPU shard vs the CPU oracle's encoding of the same global slice"}
+                  "blobs_rank0": n, "checked_blobs_per_rank": min(n, 1 << 21), "sha256_16_rank0": digest,
+                  "checked": "every rank: its GPU shard (its first 2M blobs when larger) vs the CPU oracle's "
+                             "encoding of the same global slice"}
     if rank == 0 and world == 1 and not args.no_host:
         try:
             host = host_leg(schema, make_columns(cfg, n=min(n, 1 << 22), lo=lo), dev)

@@ -15,7 +15,8 @@ import numpy as np
 
 from .columns import HostColumns
 
-__all__ = ["blob_sizes_host", "plan_shards", "slice_columns", "stitch_offsets", "config_shard"]
+__all__ = ["blob_sizes_host", "plan_shards", "plan_shards_streamed", "slice_columns", "stitch_offsets",
+           "config_shard"]
 
 
 def blob_sizes_host(schema, hc: HostColumns) -> np.ndarray:
@@ -82,18 +83,54 @@ def stitch_offsets(shard_offsets: Sequence[np.ndarray]) -> np.ndarray:
     return np.concatenate(parts)
 
 
-def config_shard(cfg, schema, per_gpu: int, world: int, rank: int) -> Tuple[int, int, int]:
+def plan_shards_streamed(piece_sizes, n: int, world: int, piece: int) -> List[Tuple[int, int]]:
+    """plan_shards over a batch whose blob sizes come in pieces
+    (piece_sizes(a, m) -> sizes of blobs [a, a + m)), in two passes of bounded
+    memory: piece totals, then the pieces that hold a boundary.  Same result
+    as plan_shards(all sizes, world)."""
+    if world <= 1 or n == 0:
+        return [(0, n)] + [(n, n)] * max(0, world - 1)
+    starts = list(range(0, n, piece))
+    sums = [int(np.asarray(piece_sizes(a, min(piece, n - a)), dtype=np.int64).sum()) for a in starts]
+    total = sum(sums)
+    bounds = [0]
+    before, k = 0, 0   # bytes before piece k
+    for r in range(1, world):
+        target = total * r / world
+        # searchsorted(cum, target, "left") = first b with cum[b] >= target
+        while k < len(starts) and before + sums[k] < target:
+            before += sums[k]
+            k += 1
+        if k == len(starts):
+            b = n
+        else:
+            sz = np.asarray(piece_sizes(starts[k], min(piece, n - starts[k])), dtype=np.int64)
+            cum = before + np.concatenate([[0], np.cumsum(sz)])
+            b = starts[k] + int(np.searchsorted(cum, target, side="left"))
+        b = min(max(b, bounds[-1]), n)
+        bounds.append(b)
+    bounds.append(n)
+    return [(bounds[r], bounds[r + 1]) for r in range(world)]
+
+
+def config_shard(cfg, schema, per_gpu: int, world: int, rank: int, piece: int = 1 << 22) -> Tuple[int, int, int]:
     """The [lo, hi) blob range rank `rank` encodes when `world` ranks split
     one global synthetic batch of world x per_gpu blobs of config `cfg`
     byte-balanced (what bench.py --gpus N runs).  Returns (lo, hi, n_global);
     the rank then generates exactly its slice with make_columns(cfg, hi - lo,
-    lo=lo)."""
-    from .configs import global_blob_sizes
+    lo=lo).  Sizes are generated `piece` blobs at a time (C5 at 8 ranks is 64M
+    blobs: the plan stays within ~100 MB of host memory per rank)."""
     n_global = per_gpu * world
     B = schema.fixed_blob_size
-    if B > 0:
-        sizes = np.full(n_global, B, dtype=np.int64)
-    else:
-        sizes = global_blob_sizes(cfg, n_global, schema.all_present_size())
-    lo, hi = plan_shards(sizes, world)[rank]
+    stat = schema.all_present_size() if B <= 0 else B
+
+    def piece_sizes(a, m):
+        if B > 0:
+            return np.full(m, B, dtype=np.int64)
+        sizes = np.full(m, stat, dtype=np.int64)
+        if cfg.var_len:
+            for _, l in cfg.var_len(m, cfg.seed, a).items():
+                sizes += np.asarray(l, dtype=np.int64)
+        return sizes
+    lo, hi = plan_shards_streamed(piece_sizes, n_global, world, piece)[rank]
     return lo, hi, n_global

@@ -125,3 +125,21 @@ def test_config_shards_like_bench(cfg_name, per_gpu, world):
     assert spans[0][0] == 0 and spans[-1][1] == n_global
     assert all(spans[r][1] == spans[r + 1][0] for r in range(world - 1))
     assert max(bytes_per) - min(bytes_per) <= 4200 * world   # byte-balanced within a blob or so
+
+
+@pytest.mark.parametrize("cfg_name,per_gpu,world,piece", [("C5", 3000, 8, 1000), ("C5", 5000, 3, 777), ("C3", 4000, 4, 1 << 22),
+                                                          ("M", 1024, 8, 100), ("C5", 10, 8, 3)])
+def test_streamed_plan_matches_full_plan(cfg_name, per_gpu, world, piece):
+    """config_shard plans C5's 64M-blob batch in bounded pieces: the streamed
+    plan must equal plan_shards over the whole size array."""
+    from packos_amd.api import CompiledSchema
+    from packos_amd.configs import CONFIGS, global_blob_sizes
+    from packos_amd.shard import config_shard, plan_shards
+    cfg = CONFIGS[cfg_name]
+    s = CompiledSchema(cfg.chain, cfg.mode)
+    n = per_gpu * world
+    B = s.fixed_blob_size
+    sizes = np.full(n, B, np.int64) if B > 0 else global_blob_sizes(cfg, n, s.all_present_size())
+    full = plan_shards(sizes, world)
+    got = [config_shard(cfg, s, per_gpu, world, r, piece=piece)[:2] for r in range(world)]
+    assert got == [tuple(x) for x in full]
