@@ -582,6 +582,7 @@ typedef __attribute__((address_space(1))) const uint64_t g_u64;
 typedef __attribute__((address_space(1))) const uint8_t g_u8;
 
 #include "encode_var.inc"
+#include "encode_gather.inc"
 #include "encode_ext.inc"
 
 // =========================================================================
@@ -2126,6 +2127,23 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
                            (uint64_t)0, out, cap, (uint64_t)n, status);
         HIP_TRY(hipGetLastError());
         return PACKOS_OK;
+    }
+    // flat closed-form chains: the chunk-gather kernel (tuning knob while it is measured)
+    if (s->tune.enc_gather && !offs_ready && !(flags & PACKOS_ENC_FORCE_GENERIC) && affine_layout(s, ec, nullptr)) {
+        GPlan G;
+        if (gather_plan(s, ec, G)) {
+            G.lits = t->enc.lits;
+            const dim3 g((unsigned)((n + kGT - 1) / kGT));
+#define PACKOS_GATHER(NV) \
+    hipLaunchKernelGGL((k_encode_gather<NV>), g, dim3(kGNT), G.lds_total, st, G, out_offsets, out, cap, (uint64_t)n, status)
+            if (G.nvar <= 1) PACKOS_GATHER(1);
+            else if (G.nvar <= 2) PACKOS_GATHER(2);
+            else if (G.nvar <= 4) PACKOS_GATHER(4);
+            else PACKOS_GATHER(8);
+#undef PACKOS_GATHER
+            HIP_TRY(hipGetLastError());
+            return PACKOS_OK;
+        }
     }
     // default: k_encode_tiles.  Data-independent presence: the kernel computes
     // (and writes) the out offsets itself, no size pass; otherwise the size pass

@@ -1,0 +1,150 @@
+"""k_encode_gather (PACKOS_ENC_GATHER=1, encode_gather.inc) vs the CPU oracle,
+bit-exact: flat closed-form chains — random leaf mixes with empty, short,
+chunk-straddling and multi-page var values, tile-edge counts, column slices
+(var offsets starting past 0), 64-bit offsets, the 13-bit overflow status and
+a capacity overrun (ErrEncode per blob that does not fit)."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle_bridge as ob
+from packos_amd import _lib
+from packos_amd.api import CompiledSchema, DeviceColumns
+from packos_amd.columns import HostColumns
+from packos_amd.configs import CONFIGS, make_columns
+from packos_amd.schema import (SBool, SBytes, SChain, SInt16, SInt32, SInt64, SStringLen, SUint8,
+                               SVariableBytes, SVariableString)
+
+pytestmark = pytest.mark.gpu
+
+LEAVES = [lambda: SBool, lambda: SUint8, lambda: SInt16, lambda: SInt32, lambda: SInt64, lambda: SStringLen(5),
+          lambda: SBytes(17), lambda: SStringLen(40)]
+LENS = [0, 1, 3, 7, 15, 16, 17, 31, 33, 80, 255, 1000, 4000]
+
+
+def torch():
+    import torch as t
+    return t
+
+
+def flat_chain(rng):
+    k = rng.randint(1, 12)
+    leaves, nvar = [], 0
+    for _ in range(k):
+        if rng.random() < 0.4 and nvar < 8:
+            leaves.append(SVariableString() if rng.random() < 0.5 else SVariableBytes())
+            nvar += 1
+        else:
+            leaves.append(rng.choice(LEAVES)())
+    if nvar == 0:
+        leaves.insert(rng.randint(0, len(leaves)), SVariableBytes())
+    return SChain(*leaves)
+
+
+def value(rng, node, lens):
+    k = node.kind
+    if k in ("int", "uint"):
+        return rng.getrandbits(8 * node.width)
+    if k == "bool":
+        return rng.random() < 0.5
+    n = node.width if node.width > 0 else rng.choice(lens)
+    if k == "string":
+        return "".join(chr(rng.randint(0x20, 0x7E)) for _ in range(n))
+    return rng.randbytes(n)
+
+
+def rows(chain, n, seed, lens=LENS):
+    rng = random.Random(seed)
+    return [[value(rng, s, lens) for s in chain.Schemas] for _ in range(n)]
+
+
+def check(chain, hc, mode, what, shift=False, off64=False):
+    T = torch()
+    s = CompiledSchema(chain, mode)
+    dc = DeviceColumns.from_host(s, hc, "cuda:0")
+    keep = []
+    for c, o in enumerate(dc.offsets):
+        if o is not None and shift:   # a column slice: offsets start past 0
+            k = 1000 + 37 * c
+            dc.data[c] = T.cat([T.full((k,), 0xEE, dtype=T.uint8, device="cuda:0"), dc.data[c]])
+            dc.offsets[c] = o + k
+    arr = dc.ctypes_array()
+    if off64:   # 64-bit offsets columns (packos_column.offsets64)
+        for c, o in enumerate(dc.offsets):
+            if o is not None:
+                o64 = o.to(T.int64).contiguous()
+                keep.append(o64)
+                arr[c].offsets = None
+                arr[c].offsets64 = o64.data_ptr()
+    a0, o0, s0 = ob.encode(chain, hc, mode, nthreads=8)
+    n = hc.n
+    L = _lib.lib()
+    out = T.zeros(int(o0[n]) + 16, dtype=T.uint8, device="cuda:0")
+    offs = T.full((n + 1,), -1, dtype=T.int64, device="cuda:0")
+    st = T.full((n,), -1, dtype=T.int32, device="cuda:0")
+    assert L.packos_encode_batch(s.handle, arr, n, out.data_ptr(), out.numel(), offs.data_ptr(), st.data_ptr(),
+                                 None, 0, 0, None) == 0, L.packos_last_error()
+    T.cuda.synchronize()
+    o1 = offs.cpu().numpy().astype(np.uint64)
+    assert np.array_equal(o1, o0), f"{what}: offsets differ"
+    a1 = out[: int(o0[n])].cpu().numpy()
+    if not np.array_equal(a0, a1):
+        bad = int(np.nonzero(a0 != a1)[0][0])
+        blob = int(np.searchsorted(o0, bad, side="right") - 1)
+        raise AssertionError(f"{what}: first diff at byte {bad} (blob {blob}, +{bad - int(o0[blob])})")
+    assert np.array_equal(st.cpu().numpy().astype(np.uint32), s0), f"{what}: status differs"
+
+
+@pytest.fixture(autouse=True)
+def gather_on(monkeypatch):
+    monkeypatch.setenv("PACKOS_ENC_GATHER", "1")   # read when the schema compiles
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_gather_random_flat(seed):
+    rng = random.Random(seed)
+    chain = flat_chain(rng)
+    n = [1, 127, 128, 129, 300, 1000, 2049][seed % 7]
+    hc = HostColumns.from_rows(chain, rows(chain, n, seed * 11 + 5))
+    check(chain, hc, seed % 2, f"seed {seed}", shift=seed % 3 == 1, off64=seed % 4 == 3)
+
+
+@pytest.mark.parametrize("lens", [[0], [0, 1], [16], [4000, 0], [7000, 9000]], ids=str)
+def test_gather_length_regimes(lens):
+    """All-empty values, 16-B values, multi-page values and blobs past the
+    13-bit header range (status PACKOS_STATUS_OVERFLOW13)."""
+    chain = SChain(SInt16, SVariableString(), SInt64, SVariableBytes(), SBool)
+    hc = HostColumns.from_rows(chain, rows(chain, 600, 99, lens))
+    check(chain, hc, 0, f"lens {lens}")
+
+
+@pytest.mark.parametrize("name,n", [("C3", 20000), ("C5", 5000)])
+def test_gather_configs(name, n):
+    cfg = CONFIGS[name]
+    check(cfg.chain, make_columns(cfg, n=n), 0, name)
+
+
+def test_gather_capacity_overrun():
+    T = torch()
+    cfg = CONFIGS["C5"]
+    hc = make_columns(cfg, n=3000)
+    a0, o0, _ = ob.encode(cfg.chain, hc, 0, nthreads=8)
+    s = CompiledSchema(cfg.chain, 0)
+    dc = DeviceColumns.from_host(s, hc, "cuda:0")
+    L = _lib.lib()
+    n = hc.n
+    for cut in (1000, int(o0[n]) // 2 + 7):
+        cap = int(o0[n]) - cut
+        out = T.zeros(cap, dtype=T.uint8, device="cuda:0")
+        offs = T.empty(n + 1, dtype=T.int64, device="cuda:0")
+        st = T.empty(n, dtype=T.int32, device="cuda:0")
+        assert L.packos_encode_batch(s.handle, dc.ctypes_array(), n, out.data_ptr(), cap, offs.data_ptr(),
+                                     st.data_ptr(), None, 0, 0, None) == 0
+        T.cuda.synchronize()
+        fits = o0[1:] <= cap
+        stn = st.cpu().numpy()
+        assert (stn[fits] == 0).all() and (stn[~fits] == 4).all()
+        last = int(o0[int(fits.sum())])
+        assert np.array_equal(out.cpu().numpy()[:last], a0[:last])
+        assert np.array_equal(offs.cpu().numpy().astype(np.uint64), o0)
