@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--op", default="encode", choices=["encode", "decode", "get"],
                    help="decode: schema.DecodeBuffer over the encoded shard; get: GetAccess GetInt of "
                         "top-level field --get-pos with the typed gather (per-config tables, not the metric)")
+    p.add_argument("--get-spans", action="store_true",
+                   help="--op get: also write start / length / tag (GetInt itself returns only value + error)")
     p.add_argument("--get-pos", type=int, default=-1,
                    help="top-level field GetInt reads (default: the config's first int64 field)")
     return p.parse_args()
@@ -433,16 +435,14 @@ def main():
 
         def get_runner(p):
             vals = torch.empty((max(n, 1), 8), dtype=torch.uint8, device=dev)
-            s0 = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
-            ln = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-            tg = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+            sps = [torch.empty(max(n, 1), dtype=dt, device=dev) for dt in (torch.int64, torch.int32, torch.uint8)]
             st = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
             offs = None if fixed else p.offsets.data_ptr()
             stride = p.B if fixed else 0
             sp = C.c_void_p(stream.cuda_stream)
+            s0, ln, tg = (t.data_ptr() for t in sps) if args.get_spans else (None, None, None)
             return lambda: L.packos_get_batch(p.out.data_ptr(), offs, stride, n, path, 1, _lib_get_int, 0, 0,
-                                              vals.data_ptr(), 8, s0.data_ptr(), ln.data_ptr(), tg.data_ptr(),
-                                              st.data_ptr(), sp)
+                                              vals.data_ptr(), 8, s0, ln, tg, st.data_ptr(), sp)
         _lib_get_int = 3   # PACKOS_GET_INT
         runs = [get_runner(p) for p in sets]
 
@@ -497,13 +497,15 @@ def main():
         gran = LINE * lines_touched(b0, end) + (0 if fixed else 8 * (n + 1)) + out_b
     elif args.op == "get":
         # GetAccess rangeAt: h0 + the two header words around the field + its
-        # payload (8 B for an int64) in; value 8 + start 8 + len 4 + tag 1 +
-        # status 1 out; + the blob offsets for var layouts
-        alg = n * (2 + 4 + 8) + n * 22 + (0 if fixed else 8 * (n + 1))
+        # payload (8 B for an int64) in; GetInt's (value, error) out = value 8 +
+        # status 1 (--get-spans: + start 8 + len 4 + tag 1); + the blob offsets
+        # for var layouts
+        wout = 22 if args.get_spans else 9
+        alg = n * (2 + 4 + 8) + n * wout + (0 if fixed else 8 * (n + 1))
         H, flds = top_layout(cfg.chain)
         pay_end = H + sum(w for _, w in flds[:args.get_pos + 1])
         end = np.minimum(b1, b0 + np.uint64(max(pay_end, 2 * args.get_pos + 4)))
-        gran = LINE * lines_touched(b0, end) + n * 22 + (0 if fixed else 8 * (n + 1))
+        gran = LINE * lines_touched(b0, end) + n * wout + (0 if fixed else 8 * (n + 1))
     blobs = n_global * args.steps
     value = blobs / el / 1e6
     achieved = alg / (kernel_ms * 1e-3) / 1e9
@@ -586,7 +588,10 @@ def main():
             "config": {"workload": f"{args.config}: {cfg.note}", "op": args.op, "blobs_per_gpu": n, "global_blobs": n_global,
                        "blob_bytes": schema.fixed_blob_size if fixed else round(total_out / n, 1),
                        "parallelism": f"dp{world} (byte-balanced disjoint shards, no collective)",
-                       "sets_rotated": len(sets), "footprint_mib": round(footprint / 2 ** 20, 1)},
+                       "sets_rotated": len(sets), "footprint_mib": round(footprint / 2 ** 20, 1),
+                       **({"get": f"GetInt(pos {args.get_pos}) -> " + ("value, start, len, tag, status" if args.get_spans
+                                                                       else "value, status")}
+                          if args.op == "get" else {})},
             "gib_per_s": round(total_out * n_global / n * args.steps / el / 2 ** 30, 2),
             "kernel_ms": round(kernel_ms, 5),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

@@ -405,6 +405,9 @@ int packos_get_field_batch(const uint8_t* arena, const uint64_t* offsets, uint64
  * getter (its LE bytes; a Bool as 0/1), or for INT the integer sign-extended
  * to int64, for FLOAT the raw bits (a float32 in the low 4 bytes); zero
  * otherwise.  value_width: want_width for FIXED / NULLABLE, 8 for INT / FLOAT.
+ * With a typed gather, out_start / out_len / out_tag may each be NULL (not
+ * written): Get<T> / GetInt / GetFloating return only (value, error); SPAN
+ * and ANY need all three.
  * status: 0 ok, 1 decode error, 2 nil nested accessor (empty container on
  * the path), 3 the reference panics (NewGetAccess returned nil and is
  * dereferenced, or GET_ANY past the field count), 4 nil value.              */

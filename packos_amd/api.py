@@ -514,7 +514,7 @@ GET_EXTENDED = 0x100   # OR-ed into a getter: read ADR-001 extended containers (
 
 
 def get_batch(arena, offsets, n: int, path, getter: int, want_tag: int = 0, want_width: int = 0,
-              stride: int = 0, values: bool = True, stream=None):
+              stride: int = 0, values: bool = True, spans: bool = True, stream=None):
     """One GetAccess getter over every blob (access/get.go:60-375):
     (values, start, length, tag, status).
 
@@ -525,24 +525,30 @@ def get_batch(arena, offsets, n: int, path, getter: int, want_tag: int = 0, want
     GET_ANY (GetTypeAndValue: any tag, end >= start; span + tag only).
     OR GET_EXTENDED into `getter` to read ADR-001 extended containers.
     `values` is an (n, value_width) uint8 tensor of the gathered typed values
-    (None for GET_SPAN or values=False); view it with .view(torch.int64) etc."""
+    (None for GET_SPAN or values=False); view it with .view(torch.int64) etc.
+    spans=False (typed gathers only) skips start / length / tag, returned as
+    None: GetInt / GetFloating / Get<T> return just (value, error)."""
     torch = _torch()
     dev = arena.device
     fam = getter & ~GET_EXTENDED   # GET_EXTENDED: read MODE_EXTENDED blobs
     vw = 8 if fam in (GET_INT, GET_FLOAT) else max(want_width, 0)
     gather = values and fam not in (GET_SPAN, GET_ANY) and vw > 0
+    if not spans and not gather:
+        raise ValueError("spans=False needs a typed gather (values=True, a FIXED/NULLABLE/INT/FLOAT getter)")
     vals = torch.empty((max(n, 1), vw), dtype=torch.uint8, device=dev) if gather else None
-    s0 = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
-    ln = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-    tg = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    s0 = torch.empty(max(n, 1), dtype=torch.int64, device=dev) if spans else None
+    ln = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if spans else None
+    tg = torch.empty(max(n, 1), dtype=torch.uint8, device=dev) if spans else None
     st = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
     p = (C.c_int32 * len(path))(*path)
+    ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
     check(lib().packos_get_batch(arena.data_ptr(), None if offsets is None else offsets.data_ptr(), stride, n,
                                  p, len(path), getter, want_tag, want_width,
-                                 None if vals is None else vals.data_ptr(), vw if gather else 0,
-                                 s0.data_ptr(), ln.data_ptr(), tg.data_ptr(), st.data_ptr(), _stream_ptr(stream)),
+                                 ptr(vals), vw if gather else 0,
+                                 ptr(s0), ptr(ln), ptr(tg), st.data_ptr(), _stream_ptr(stream)),
           "packos_get_batch")
-    return (None if vals is None else vals[:n]), s0[:n], ln[:n], tg[:n], st[:n]
+    cut = lambda t: None if t is None else t[:n]  # noqa: E731
+    return cut(vals), cut(s0), cut(ln), cut(tg), st[:n]
 
 
 def get_map_batch(arena, offsets, n: int, path, flags: int = MAP_STR, max_pairs: int = 8, stride: int = 0,

@@ -1521,9 +1521,11 @@ __global__ __launch_bounds__(kBlock) void k_get_field(const uint8_t* __restrict_
             }
         }
     }
-    out_start[i] = o_start;
-    out_len[i] = o_len;
-    out_tag[i] = (uint8_t)o_tag;
+    // the span / tag outputs are optional: GetInt / GetFloating / Get<T>
+    // return only (value, error), so a typed gather may skip them
+    if (out_start) out_start[i] = o_start;
+    if (out_len) out_len[i] = o_len;
+    if (out_tag) out_tag[i] = (uint8_t)o_tag;
     status[i] = (uint8_t)rc;
     if (!out_values) return;
     uint8_t* dst = out_values + i * value_width;
@@ -2333,11 +2335,15 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
 int packos_get_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t stride, size_t n, const int32_t* path,
                      int depth, int getter, int want_tag, int want_width, uint8_t* out_values, uint32_t value_width,
                      uint64_t* out_start, uint32_t* out_len, uint8_t* out_tag, uint8_t* status, void* stream) {
-    if (!path || depth < 1 || depth > 16 || !out_start || !out_len || !out_tag || !status || (!arena && n))
-        return PACKOS_E_INVALID;
+    if (!path || depth < 1 || depth > 16 || !status || (!arena && n)) return PACKOS_E_INVALID;
     const int g_base = getter & ~PACKOS_GET_EXTENDED;
     if (g_base < PACKOS_GET_FIXED || g_base > PACKOS_GET_ANY) {
         set_error("unknown getter");
+        return PACKOS_E_INVALID;
+    }
+    // spans may be skipped only where a typed value carries the result
+    if ((!out_start || !out_len || !out_tag) && (g_base == PACKOS_GET_SPAN || g_base == PACKOS_GET_ANY || !out_values)) {
+        set_error("out_start / out_len / out_tag may be NULL only for a typed gather (out_values set)");
         return PACKOS_E_INVALID;
     }
     if (out_values && value_width == 0) {

@@ -13,7 +13,7 @@ import oracle_bridge as ob
 from packos_amd import _lib
 from golden_util import MODES, chain_of, load, unwrap
 from packos_amd.api import (CompiledSchema, DeviceColumns, decode_batch, encode_batch, get_batch, get_field_batch,
-                           get_map_batch)
+                           get_map_batch, GET_ANY, GET_INT, GET_SPAN)
 from packos_amd.columns import HostColumns
 from packos_amd.configs import CONFIGS, make_columns
 from packos_amd.schema import SBool, SChain, SInt16, SInt32, SInt64, SStringLen, SVariableString, STuple, SMap, SString
@@ -848,6 +848,28 @@ def test_random_get_batch(seed):
             assert g[0] is None
         else:
             assert np.array_equal(o[0], g[0]), what
+            # GetInt-style call: value + status only, spans not written
+            v = get_batch(da, do, hc.n, path, getter, tag, width, spans=False)
+            assert v[1] is None and v[2] is None and v[3] is None
+            assert np.array_equal(o[0], v[0].cpu().numpy()), what
+            assert np.array_equal(o[4], v[4].cpu().numpy()), what
+
+
+def test_get_batch_spans_required_without_gather():
+    """spans=False is refused where no typed value carries the result (SPAN,
+    ANY, values=False): the C ABI returns PACKOS_E_INVALID."""
+    T = torch()
+    da = T.zeros(64, dtype=T.uint8, device="cuda:0")
+    for getter in (GET_SPAN, GET_ANY):
+        with pytest.raises(ValueError):
+            get_batch(da, None, 4, [0], getter, 0, 0, stride=16, spans=False)
+    with pytest.raises(ValueError):
+        get_batch(da, None, 4, [0], GET_INT, 0, 0, stride=16, values=False, spans=False)
+    st = T.zeros(4, dtype=T.uint8, device="cuda:0")
+    path = (C.c_int32 * 1)(0)
+    rc = _lib.lib().packos_get_batch(da.data_ptr(), None, 16, 4, path, 1, GET_SPAN, 0, 0, None, 0,
+                                     None, None, None, st.data_ptr(), None)
+    assert rc == -1   # PACKOS_E_INVALID
 
 
 def test_get_batch_nullable_and_any_width():
