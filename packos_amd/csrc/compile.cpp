@@ -828,7 +828,7 @@ void read_tune(Tune& t) {
     t.sizes_scan = getenv("PACKOS_SIZES_SCAN") != nullptr;
     t.decode_generic = getenv("PACKOS_DECODE_GENERIC") != nullptr;
     if (const char* e = getenv("PACKOS_DEC_TILE_BYTES")) t.dec_tile_bytes = std::min(49152, std::max(1024, atoi(e)));
-    if (const char* e = getenv("PACKOS_ENC_GATHER")) t.enc_gather = atoi(e);
+    if (const char* e = getenv("PACKOS_ENC_FLAT")) t.enc_flat = atoi(e);
 }
 
 // Same rule as the device's ext_layout_wave (kernels.hip): containers in

@@ -582,7 +582,7 @@ typedef __attribute__((address_space(1))) const uint64_t g_u64;
 typedef __attribute__((address_space(1))) const uint8_t g_u8;
 
 #include "encode_var.inc"
-#include "encode_gather.inc"
+#include "encode_flat.inc"
 #include "encode_ext.inc"
 
 // =========================================================================
@@ -2130,19 +2130,23 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
         HIP_TRY(hipGetLastError());
         return PACKOS_OK;
     }
-    // flat closed-form chains: the chunk-gather kernel (tuning knob while it is measured)
-    if (s->tune.enc_gather && !offs_ready && !(flags & PACKOS_ENC_FORCE_GENERIC) && affine_layout(s, ec, nullptr)) {
-        GPlan G;
-        if (gather_plan(s, ec, G)) {
-            G.lits = t->enc.lits;
-            const dim3 g((unsigned)((n + kGT - 1) / kGT));
-#define PACKOS_GATHER(NV) \
-    hipLaunchKernelGGL((k_encode_gather<NV>), g, dim3(kGNT), G.lds_total, st, G, out_offsets, out, cap, (uint64_t)n, status)
-            if (G.nvar <= 1) PACKOS_GATHER(1);
-            else if (G.nvar <= 2) PACKOS_GATHER(2);
-            else if (G.nvar <= 4) PACKOS_GATHER(4);
-            else PACKOS_GATHER(8);
-#undef PACKOS_GATHER
+    // flat closed-form chains of large blobs: k_encode_flat (encode_flat.inc).
+    // Small blobs stay on k_encode_tiles, whose frame builds the whole output
+    // image in LDS (C3, 85-B blobs: 0.060 ms there vs 0.106 ms here); large
+    // blobs stream their values straight from HBM here (C5, 969-B blobs: 3.97
+    // ms vs 4.29).  The blob sizes are device data: `cap` (the arena the caller
+    // sized, normally from packos_encoded_size_batch) stands in for them.
+    const bool flat_ok = s->tune.enc_flat == 1 || (s->tune.enc_flat == 2 && n && cap / n >= kFlatMinBlob);
+    if (flat_ok && !offs_ready && !(flags & PACKOS_ENC_FORCE_GENERIC) && affine_layout(s, ec, nullptr)) {
+        FPlan F;
+        if (flat_plan(s, ec, F)) {
+            const dim3 g((unsigned)((n + kFT - 1) / kFT));
+#define PACKOS_FLAT(NV) \
+    hipLaunchKernelGGL((k_encode_flat<NV>), g, dim3(kFNT), F.lds_total, st, F, out_offsets, out, cap, (uint64_t)n, status)
+            if (F.nvar <= 1) PACKOS_FLAT(1);
+            else if (F.nvar <= 2) PACKOS_FLAT(2);
+            else PACKOS_FLAT(4);
+#undef PACKOS_FLAT
             HIP_TRY(hipGetLastError());
             return PACKOS_OK;
         }

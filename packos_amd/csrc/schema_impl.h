@@ -38,14 +38,15 @@ struct Node {
 // variable-size encoder), PACKOS_SIZES_SCAN=1 (look-back size kernel even for
 // closed-form layouts), PACKOS_DECODE_GENERIC=1 (thread-per-blob decoder even
 // for fixed layouts), PACKOS_DEC_TILE_BYTES (staged bytes per fixed-decode
-// tile), PACKOS_TILE_BYTES (fixed-encode tile bytes), PACKOS_ENC_GATHER
-// (chunk-gather var encoder for flat closed-form chains).
+// tile), PACKOS_TILE_BYTES (fixed-encode tile bytes), PACKOS_ENC_FLAT
+// (flat closed-form var encoder k_encode_flat: 0 never, 1 always, 2 = auto:
+// when the output capacity averages >= 256 B per blob).
 struct Tune {
     int var_per = 40;
     bool sizes_scan = false;
     bool decode_generic = false;
     int dec_tile_bytes = 0;      // 0: 24 KB for B >= 128, else 16 KB
-    int enc_gather = 0;          // PACKOS_ENC_GATHER=1: flat closed-form chains take k_encode_gather
+    int enc_flat = 2;            // PACKOS_ENC_FLAT: 0 never, 1 always, 2 auto (large blobs)
 };
 
 struct DeviceTables {

@@ -1,5 +1,5 @@
-"""k_encode_gather (PACKOS_ENC_GATHER=1, encode_gather.inc) vs the CPU oracle,
-bit-exact: flat closed-form chains — random leaf mixes with empty, short,
+"""k_encode_flat (encode_flat.inc, the default for flat closed-form chains)
+vs the CPU oracle, bit-exact: flat closed-form chains — random leaf mixes with empty, short,
 chunk-straddling and multi-page var values, tile-edge counts, column slices
 (var offsets starting past 0), 64-bit offsets, the 13-bit overflow status and
 a capacity overrun (ErrEncode per blob that does not fit)."""
@@ -97,12 +97,12 @@ def check(chain, hc, mode, what, shift=False, off64=False):
 
 
 @pytest.fixture(autouse=True)
-def gather_on(monkeypatch):
-    monkeypatch.setenv("PACKOS_ENC_GATHER", "1")   # read when the schema compiles
+def flat_on(monkeypatch):
+    monkeypatch.setenv("PACKOS_ENC_FLAT", "1")   # read when the schema compiles
 
 
 @pytest.mark.parametrize("seed", range(40))
-def test_gather_random_flat(seed):
+def test_flat_random_flat(seed):
     rng = random.Random(seed)
     chain = flat_chain(rng)
     n = [1, 127, 128, 129, 300, 1000, 2049][seed % 7]
@@ -111,7 +111,7 @@ def test_gather_random_flat(seed):
 
 
 @pytest.mark.parametrize("lens", [[0], [0, 1], [16], [4000, 0], [7000, 9000]], ids=str)
-def test_gather_length_regimes(lens):
+def test_flat_length_regimes(lens):
     """All-empty values, 16-B values, multi-page values and blobs past the
     13-bit header range (status PACKOS_STATUS_OVERFLOW13)."""
     chain = SChain(SInt16, SVariableString(), SInt64, SVariableBytes(), SBool)
@@ -119,13 +119,19 @@ def test_gather_length_regimes(lens):
     check(chain, hc, 0, f"lens {lens}")
 
 
+@pytest.mark.parametrize("flat", ["1", "0"])
 @pytest.mark.parametrize("name,n", [("C3", 20000), ("C5", 5000)])
-def test_gather_configs(name, n):
+def test_flat_configs(name, n, flat, monkeypatch):
+    """The configs through k_encode_flat and (PACKOS_ENC_FLAT=0) through
+    k_encode_tiles, both modes."""
+    monkeypatch.setenv("PACKOS_ENC_FLAT", flat)
     cfg = CONFIGS[name]
-    check(cfg.chain, make_columns(cfg, n=n), 0, name)
+    hc = make_columns(cfg, n=n)
+    for mode in (0, 1):
+        check(cfg.chain, hc, mode, f"{name} flat={flat} mode {mode}")
 
 
-def test_gather_capacity_overrun():
+def test_flat_capacity_overrun():
     T = torch()
     cfg = CONFIGS["C5"]
     hc = make_columns(cfg, n=3000)
