@@ -1070,11 +1070,17 @@ __device__ __forceinline__ uint32_t decode_flat_k(const FlatArg& A, const R& r, 
 // falling back to HBM only beyond it.  Replaces ~one dependent global byte
 // load per header word / payload byte with one load round.
 constexpr int kDecWinChunks = 8;
+#ifndef PACKOS_DECWIN_ATTR
+#define PACKOS_DECWIN_ATTR
+#endif
+#ifndef PACKOS_DECFIX_ATTR
+#define PACKOS_DECFIX_ATTR
+#endif
 
 // WC: window chunks per blob — enough for the schema's static prefix (bytes
 // before the first var payload; compile.cpp), at most kDecWinChunks.
 template <int WC, bool EXT>
-__global__ __launch_bounds__(kBlock) void k_decode_win(DecProgram P, DecCols cols, FlatArg FA,
+__global__ __launch_bounds__(kBlock) PACKOS_DECWIN_ATTR void k_decode_win(DecProgram P, DecCols cols, FlatArg FA,
                                                        const uint8_t* __restrict__ arena,
                                                        const uint64_t* __restrict__ offs, uint64_t stride, uint64_t n,
                                                        uint32_t* __restrict__ status) {
@@ -1188,7 +1194,7 @@ struct DecColsK {
 __device__ __forceinline__ uint32_t lds_u8(const uint32_t* lds, uint32_t a) { return (lds[a >> 2] >> (8 * (a & 3))) & 0xFFu; }
 
 template <bool EXT>
-__global__ __launch_bounds__(kBlock) void k_decode_fixed(DecFixProgram F, DecProgram P, DecCols cols, DecColsK K,
+__global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecFixProgram F, DecProgram P, DecCols cols, DecColsK K,
                                                          const uint8_t* __restrict__ arena,
                                                          const uint64_t* __restrict__ offs, uint64_t n,
                                                          uint32_t* __restrict__ status) {
