@@ -1056,6 +1056,8 @@ __device__ __forceinline__ uint32_t decode_flat_k(const FlatArg& A, const R& r, 
         else if (fw == 2) *(g16*)dp = (uint16_t)r.u16(pay);
         else if (fw == 4) *(g32*)dp = r.u32(pay);
         else if (fw == 8) *(g64*)dp = (uint64_t)r.u32(pay) | ((uint64_t)r.u32(pay + 4) << 32);
+        else if (fw == 16 && ((uintptr_t)dp & 15) == 0)   // one 16-B store (lanes 16 B apart: whole lines)
+            *(__attribute__((address_space(1))) u32x4*)dp = u32x4{r.u32(pay), r.u32(pay + 4), r.u32(pay + 8), r.u32(pay + 12)};
         else if ((fw & 3) == 0)
             for (int x = 0; x < fw; x += 4) *(g32*)(dp + x) = r.u32(pay + x);
         else
@@ -1457,8 +1459,13 @@ __global__ __launch_bounds__(kBlock) void k_get_field(const uint8_t* __restrict_
     r.n = bl >= 32 ? 32u : bl >= 16 ? 16u : 0u;
     {
         const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+#ifdef PACKOS_GET_NT
+        const u32x4 w0 = r.n >= 16 ? __builtin_nontemporal_load((const g_u32x4*)(arena + a0)) : z;
+        const u32x4 w1 = r.n >= 32 ? __builtin_nontemporal_load((const g_u32x4*)(arena + a0 + 16)) : z;
+#else
         const u32x4 w0 = r.n >= 16 ? *(const g_u32x4*)(arena + a0) : z;
         const u32x4 w1 = r.n >= 32 ? *(const g_u32x4*)(arena + a0 + 16) : z;
+#endif
         r.W[0] = w0.x; r.W[1] = w0.y; r.W[2] = w0.z; r.W[3] = w0.w;
         r.W[4] = w1.x; r.W[5] = w1.y; r.W[6] = w1.z; r.W[7] = w1.w;
     }
@@ -1598,8 +1605,13 @@ __global__ __launch_bounds__(kBlock) void k_get_map(const uint8_t* __restrict__ 
     r.n = bl >= 32 ? 32u : bl >= 16 ? 16u : 0u;
     {
         const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+#ifdef PACKOS_GET_NT
+        const u32x4 w0 = r.n >= 16 ? __builtin_nontemporal_load((const g_u32x4*)(arena + a0)) : z;
+        const u32x4 w1 = r.n >= 32 ? __builtin_nontemporal_load((const g_u32x4*)(arena + a0 + 16)) : z;
+#else
         const u32x4 w0 = r.n >= 16 ? *(const g_u32x4*)(arena + a0) : z;
         const u32x4 w1 = r.n >= 32 ? *(const g_u32x4*)(arena + a0 + 16) : z;
+#endif
         r.W[0] = w0.x; r.W[1] = w0.y; r.W[2] = w0.z; r.W[3] = w0.w;
         r.W[4] = w1.x; r.W[5] = w1.y; r.W[6] = w1.z; r.W[7] = w1.w;
     }
