@@ -170,3 +170,26 @@ def test_has_checks():
     assert CompiledSchema(json.dumps([{"type": "int16", "min": 0, "max": 9}])).has_checks
     assert CompiledSchema(json.dumps([{"type": "string", "prefix": "ab"}])).has_checks
     assert not CompiledSchema(json.dumps([{"type": "string", "decodeDefault": "x"}])).has_checks
+
+
+def test_get_batch_span_outputs_optional_only_for_typed_gathers():
+    """packos_get_batch argument rules, checked before any device work (n = 0):
+    start / len / tag may be NULL only when a typed value (out_values) carries
+    the result; SPAN / ANY / no gather with NULL spans -> PACKOS_E_INVALID."""
+    L = _lib.lib()
+    path = (C.c_int32 * 1)(0)
+    st = (C.c_uint8 * 4)()
+    vals = (C.c_uint8 * 32)()
+    s0 = (C.c_uint64 * 4)()
+    ln = (C.c_uint32 * 4)()
+    tg = (C.c_uint8 * 4)()
+    arena = (C.c_uint8 * 16)()
+    GET_SPAN, GET_INT, GET_ANY = 2, 3, 5
+    call = lambda g, v, spans: L.packos_get_batch(arena, None, 16, 0, path, 1, g, 0, 0, v, 8 if v else 0,  # noqa: E731
+                                                  *((s0, ln, tg) if spans else (None, None, None)), st, None)
+    assert call(GET_INT, vals, False) == 0
+    assert call(GET_INT, vals, True) == 0
+    assert call(GET_SPAN, None, True) == 0
+    assert call(GET_SPAN, None, False) == -1
+    assert call(GET_ANY, None, False) == -1
+    assert call(GET_INT, None, False) == -1
