@@ -1547,7 +1547,7 @@ __global__ __launch_bounds__(kBlock) void k_get_field(const uint8_t* __restrict_
     }
     // the span / tag outputs are optional: GetInt / GetFloating / Get<T>
     // return only (value, error), so a typed gather may skip them
-#ifdef PACKOS_GET_NTS
+#ifndef PACKOS_GET_PLAIN   // non-temporal: M GetInt 0.0276 -> 0.0266 ms, C5 0.248 -> 0.244 (A/B on the box)
     if (out_start) __builtin_nontemporal_store(o_start, out_start + i);
     if (out_len) __builtin_nontemporal_store(o_len, out_len + i);
     if (out_tag) __builtin_nontemporal_store((uint8_t)o_tag, out_tag + i);
@@ -1561,7 +1561,7 @@ __global__ __launch_bounds__(kBlock) void k_get_field(const uint8_t* __restrict_
     if (!out_values) return;
     uint8_t* dst = out_values + i * value_width;
     if (value_width == 8 && ((uintptr_t)dst & 7) == 0) {
-#ifdef PACKOS_GET_NTS
+#ifndef PACKOS_GET_PLAIN
         __builtin_nontemporal_store(val, (uint64_t*)dst);
 #else
         *(uint64_t*)dst = val;
