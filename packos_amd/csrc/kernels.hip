@@ -1178,7 +1178,11 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECWIN_ATTR void k_decode_win(DecPro
         sv = decode_flat(LP, cols, R, a0, a1, i);
     }
     if (sv == kFlatFallback) sv = decode_blob<WReader, EXT>(LP, cols, R, a0, a1, i);
+#ifdef PACKOS_DEC_STNT
+    __builtin_nontemporal_store(sv, status + i);
+#else
     status[i] = sv;
+#endif
 }
 
 // Fixed-layout decode (the transpose of k_encode_fixed_dw).  A workgroup
@@ -1359,7 +1363,11 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
         if (fail[j])
             sv = decode_blob<GReader, EXT>(P, cols, GReader{arena}, offs ? offs[i] : i * B,
                                            offs ? offs[i + 1] : (i + 1) * B, i);
+#ifdef PACKOS_DEC_STNT
+        __builtin_nontemporal_store(sv, status + i);
+#else
         status[i] = sv;
+#endif
     }
 }
 
