@@ -461,6 +461,11 @@ int packos_get_map_batch(const uint8_t* arena, const uint64_t* offsets, uint64_t
 const char* packos_strerror(int code);
 const char* packos_last_error(void);   /* thread-local detail of the last failure */
 int         packos_abi_version(void);
+/* Diagnostics: the encode kernel the last packos_encode_batch call of this
+ * thread launched ("fixed_tile", "fixed_dw", "fixed", "var", "ext", "flat",
+ * "tiles", "" before any call).  No reference counterpart; tests use it to
+ * assert which encoder a batch exercised.                                      */
+const char* packos_last_encoder(void);
 
 #ifdef __cplusplus
 }

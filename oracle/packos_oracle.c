@@ -410,21 +410,30 @@ int64_t or_encoded_size_one(const or_schema* s, const packos_column* cols, size_
     return sz;
 }
 
-/* EncodeFunc value checks in emission order: the first failing leaf's own
- * ErrorCode (Range -> ErrOutOfRange, SDateRange -> ErrDateOutOfRange,
- * CheckFunc -> ErrEncode), 0 if every value passes.  Nil containers and nil
- * values are not encoded, so not checked (schema.go:1203-1214, 2227-2246,
- * 1110-1124).                                                                */
+/* EncodeFunc value checks in emission order: the ErrorCode of the first
+ * failing top-level field (Range -> ErrOutOfRange, SDateRange ->
+ * ErrDateOutOfRange, CheckFunc -> ErrEncode; a present TupleSchemaNamed whose
+ * FieldNames and Schemas differ in length -> ErrConstraintViolated,
+ * schema.go:1808-1810), 0 if every value passes.  A tuple or map wraps its
+ * child's error as ErrInvalidFormat (schema.go:1671-1673, 1859-1861,
+ * 444-449).  Nil containers and nil values are not encoded, so not checked
+ * (schema.go:1203-1214, 2227-2246, 1110-1124, 1804-1806).                    */
+static int has_names_bad(const or_schema* s) {
+    for (int n = 0; n < s->n_nodes; n++)
+        if (NK(s, n) == ORN_TUPLE && (NC(s, n) & ORT_NAMES_BAD)) return 1;
+    return 0;
+}
+
 static int enc_check(const or_schema* s, const packos_column* cols, size_t i, int n) {
     int k = NK(s, n);
     if (is_container(k)) {
         int nullable = (k == ORN_MAP) ? 1 : NA(s, n);
         if (nullable && !col_valid(&cols[s->col_of_node[n]], i)) return 0;
+        if (k == ORN_TUPLE && (NC(s, n) & ORT_NAMES_BAD)) return 3;
         int kids[256];
         int nk = children(s, n, kids);
         for (int j = 0; j < nk; j++) {
-            int r = enc_check(s, cols, i, kids[j]);
-            if (r) return r;
+            if (enc_check(s, cols, i, kids[j])) return 1;
         }
         return 0;
     }
@@ -515,7 +524,8 @@ static void* enc_worker(void* arg) {
         encode_one_tls(j->s, j->cols, i, j->mode, j->out + j->offs[i], cap, &o, &t);
         if (j->status) {
             uint32_t sv = o ? PACKOS_STATUS_OVERFLOW13 : 0u;
-            for (int tp = 0; j->s->ext && tp < j->s->n_top; tp++) {
+            const int chk = j->s->ext != NULL || has_names_bad(j->s);
+            for (int tp = 0; chk && tp < j->s->n_top; tp++) {
                 int inner = enc_check(j->s, j->cols, i, j->s->top_nodes[tp]);
                 if (inner) {
                     /* SchemaError(ErrEncode, ChainName, "", -1, err): position -1 (schema.go:919-936) */
@@ -675,6 +685,7 @@ typedef struct dec_ctx {
 } dec_ctx;
 
 #define DEC_PANIC 0x100
+#define DEC_POS0 0x200   /* the error carries position 0, not the field's */
 
 /* precheck (schema.go:997-1013): 0 ok, else ErrConstraintViolated */
 static int precheck(const or_seq* q, int tag, int64_t hint, int nullable, int64_t* w) {
@@ -756,6 +767,9 @@ static int dec_node(dec_ctx* c, int n, or_seq* q, uint64_t sub_base) {
             return 0;
         }
         case ORN_TUPLE: case ORN_MAP: {
+            /* TupleSchemaNamed.Decode: len(FieldNames) != len(Schemas) fails first,
+             * ErrConstraintViolated at position 0 (schema.go:1754-1756)            */
+            if (k == ORN_TUPLE && (NC(s, n) & ORT_NAMES_BAD)) return 3 | DEC_POS0;
             int nul = (k == ORN_MAP) ? 1 : NA(s, n);
             int xc = c->ext && q->cur_type == PACKOS_TAG_EXTENDED;
             int e = precheck(q, xc ? PACKOS_TAG_EXTENDED : leaf_tag(k), -1, nul, &w);
@@ -771,7 +785,11 @@ static int dec_node(dec_ctx* c, int n, or_seq* q, uint64_t sub_base) {
                 } else if (or_seq_peek_nested(q, &sub)) {
                     return 1;
                 }
-                if (k == ORN_TUPLE && nk > 0 && (sub.count - 1) != nk && !NC(s, n)) return 3;
+                /* arg count: TupleSchema.Decode checks it only when argCount > 0
+                 * (schema.go:1607), TupleSchemaNamed.Decode always (:1773)       */
+                if (k == ORN_TUPLE && !(NC(s, n) & ORT_VARIABLE) && (nk > 0 || (NC(s, n) & ORT_NAMED)) &&
+                    (sub.count - 1) != nk)
+                    return 3;
                 uint64_t nb = sub_base + (uint64_t)q->cur_off;
                 for (int j = 0; j < nk; j++) {
                     int ce = dec_node(c, kids[j], &sub, nb);
@@ -801,6 +819,7 @@ static uint32_t decode_one(const or_schema* s, const uint8_t* blob, int64_t len,
     for (int t = 0; t < s->n_top; t++) {
         int e = dec_node(&c, s->top_nodes[t], &q, base);
         if (e == DEC_PANIC) return PACKOS_STATUS_PANIC | ((uint32_t)(t + 1) << 8);
+        if (e & DEC_POS0) return (uint32_t)(e & 0xFF) | (1u << 8);
         if (e) return (uint32_t)e | ((uint32_t)(t + 1) << 8);
     }
     return 0;

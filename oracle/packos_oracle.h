@@ -60,8 +60,14 @@ enum {
     ORN_STRING = 5, /* a = SchemaString.Width (0 nullable, >0 exact, -1 optional) */
     ORN_BYTES = 6,  /* a = SchemaBytes.Width */
     ORN_MATCH = 7,  /* a = literal index, b = SchemaString Width (SString.Match / map key) */
-    ORN_TUPLE = 8,  /* a = nullable, b = nchild, c = variableLength */
+    ORN_TUPLE = 8,  /* a = nullable, b = nchild, c = ORT_* flags */
     ORN_MAP = 9     /* a = sorted,   b = nchild (key,value,...) */
+};
+/* ORN_TUPLE c flags */
+enum {
+    ORT_VARIABLE = 1,      /* VariableLength: no arg-count check                */
+    ORT_NAMED = 2,         /* TupleSchemaNamed: the check has no argCount > 0 guard */
+    ORT_NAMES_BAD = 4      /* TupleSchemaNamed with len(FieldNames) != len(Schemas) */
 };
 
 typedef struct or_schema {

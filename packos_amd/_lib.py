@@ -39,6 +39,7 @@ EXPORTED = [
     "packos_encoded_size_batch", "packos_encode_batch", "packos_encode_host_batch", "packos_decode_host_batch", "packos_decode_batch",
     "packos_pipeline_create", "packos_pipeline_free", "packos_pipeline_encode", "packos_pipeline_decode",
     "packos_get_field_batch", "packos_get_batch", "packos_get_map_batch", "packos_strerror", "packos_last_error", "packos_abi_version",
+    "packos_last_encoder",
 ]
 
 
@@ -117,6 +118,7 @@ def lib():
     L.packos_strerror.argtypes = [i32]
     L.packos_strerror.restype = C.c_char_p
     L.packos_last_error.restype = C.c_char_p
+    L.packos_last_encoder.restype = C.c_char_p
     L.packos_abi_version.restype = i32
     got = L.packos_abi_version()
     if got != ABI_VERSION:   # a stale or foreign .so would read packos_column with the wrong stride

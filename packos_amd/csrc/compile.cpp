@@ -246,6 +246,14 @@ struct Builder {
                 // schema.go:1551-1552)
                 n.nullable = true;
                 n.variable = bool_field(j, "variableLength");
+                // BuildSchema makes a TupleSchemaNamed of a non-empty fieldNames
+                // (schemabuilder_json.go:245-253); "named" (a key of this build,
+                // which Go's json ignores) marks STupleNamed(nil, ...) / an empty
+                // name list, which the reference JSON cannot express
+                const size_t nn = names && names->kind == JVal::ARR ? names->arr.size() : 0;
+                n.named = nn > 0 || bool_field(j, "named");
+                const size_t ns = sch && sch->kind == JVal::ARR ? sch->arr.size() : 0;
+                n.names_bad = n.named && nn != ns;
             }
             if (sch && sch->kind == JVal::ARR) {
                 for (size_t k = 0; k < sch->arr.size(); k++) {
@@ -413,6 +421,18 @@ struct Builder {
                 if (can_nil) s->has_nullable = true;
                 int cid = (int)s->conts.size();
                 s->conts.push_back(c);
+                if (n.kind == K_TUPLE && n.names_bad) {
+                    // TupleSchemaNamed.Encode of a present value fails before writing
+                    // anything (schema.go:1808-1810); a parent tuple / map wraps it as
+                    // ErrInvalidFormat
+                    EncCheck k{};
+                    k.col = n.col;
+                    k.cont = cid;
+                    k.top = n.top;
+                    k.flags = CHK_FAIL;
+                    k.inner = cont_id == 0 ? PACKOS_ERR_CONSTRAINT_VIOLATED : PACKOS_ERR_INVALID_FORMAT;
+                    s->echk.push_back(k);
+                }
                 emit_container(id, cid);
                 return;
             }
@@ -443,6 +463,9 @@ struct Builder {
         } else {
             c.inner = (n.check & CHK_DATE) ? PACKOS_ERR_DATE_OUT_OF_RANGE : PACKOS_ERR_OUT_OF_RANGE;
         }
+        // a leaf inside a tuple / map: the container wraps its error as
+        // ErrInvalidFormat (schema.go:1671-1673, 1859-1861, 444-449)
+        if (cont_id != 0) c.inner = PACKOS_ERR_INVALID_FORMAT;
         s->echk.push_back(c);
     }
 
@@ -588,6 +611,7 @@ struct Builder {
         }
         s->dvchk.clear();
         for (const EncCheck& c : s->echk) {
+            if (c.flags & CHK_FAIL) continue;   // no value to check (the decoder fails the blob itself)
             DecChk v{};
             for (const DecFix& df : s->dfix)
                 if (df.col == c.col) v.blob_off = df.blob_off;
@@ -744,7 +768,8 @@ struct Builder {
             d.kid0 = (int)s->dkids.size();
             for (int k : n.kids) s->dkids.push_back(k);
             d.tag = (uint8_t)tag_of(n.kind);
-            d.variable = n.variable;
+            d.variable = (uint8_t)((n.variable ? DT_VARIABLE : 0) | (n.named ? DT_NAMED : 0) |
+                                   (n.names_bad ? DT_NAMES_BAD : 0));
             switch (n.kind) {
                 case K_STRING: case K_BYTES: case K_MATCH: d.nullable = n.width <= 0; break;
                 case K_MAP: d.nullable = 1; break;
@@ -903,6 +928,12 @@ int packos_schema_compile(const char* schema_json, int mode, packos_schema** out
             list = j.get("schema");
             names = j.get("fieldNames");
             if (!list || list->kind != JVal::ARR) fail(PACKOS_E_SCHEMA, "chain needs a schema array");
+            // SchemaNamedChain whose FieldNames and Schemas differ in length:
+            // DecodeBufferNamed fails every blob, EncodeValueNamed writes only
+            // len(FieldNames) fields or indexes past Schemas (schema.go:953-956,
+            // 975-994) — fenced off here
+            if (names && names->kind == JVal::ARR && !names->arr.empty() && names->arr.size() != list->arr.size())
+                fail(PACKOS_E_SCHEMA, "SchemaNamedChain: fieldNames and schema differ in length");
         } else if (j.kind == JVal::OBJ) {
             single.kind = JVal::ARR;
             single.arr.push_back(j);

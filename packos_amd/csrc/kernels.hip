@@ -543,7 +543,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_checks(const EncCheck* __rest
         const EncCheck c = chk[k];
         if (!((pm >> c.cont) & 1ull)) continue;
         bool bad;
-        if (c.flags & CHK_RANGE) {
+        if (c.flags & CHK_FAIL) {
+            bad = true;   // the container is present: its Encode fails whatever the value
+        } else if (c.flags & CHK_RANGE) {
             const uint8_t* v = cols.valid[c.col];
             if (v && !v[i]) continue;
             const uint8_t* p = cols.data[c.col] + i * (uint64_t)c.width;
@@ -720,6 +722,7 @@ __host__ __device__ __forceinline__ int dprecheck(const DSeq& s, int tag, int64_
 }
 
 constexpr int kPanic = 0x100;
+constexpr int kPos0 = 0x200;   // the error's position is 0, not the field's (schema.go:1756-1758)
 
 // w bytes from reader position p to a column row; dword stores when aligned
 template <class R>
@@ -775,6 +778,7 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
         DSeq& q = cur.q;
         int64_t w = 0;
         if (nd.kind == K_TUPLE || nd.kind == K_MAP) {
+            if (nd.kind == K_TUPLE && (nd.variable & DT_NAMES_BAD)) { err = 3 | kPos0; break; }
             const bool xc = EXT && q.cur_type == PACKOS_TAG_EXTENDED;   // an extended container field
             err = dprecheck(q, xc ? PACKOS_TAG_EXTENDED : nd.tag, -1, nd.nullable, w);
             if (err) break;
@@ -788,7 +792,10 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
                     err = 1;
                     break;
                 }
-                if (nd.kind == K_TUPLE && nd.nkids > 0 && (c.q.count - 1) != nd.nkids && !nd.variable) {
+                // arg count: TupleSchema checks it only when argCount > 0
+                // (schema.go:1607), TupleSchemaNamed always (:1773)
+                if (nd.kind == K_TUPLE && !(nd.variable & DT_VARIABLE) && (nd.nkids > 0 || (nd.variable & DT_NAMED)) &&
+                    (c.q.count - 1) != nd.nkids) {
                     err = 3;
                     break;
                 }
@@ -873,7 +880,8 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
     uint32_t sv = 0;
     if (err) {
         const uint32_t posv = (uint32_t)((d == 0 ? cur.k : stk[0].k) + 1) << 8;
-        if (err == kPanic) sv = PACKOS_STATUS_PANIC | posv;
+        if (err & kPos0) sv = d == 0 ? (uint32_t)(err & 0xFF) | (1u << 8) : (uint32_t)PACKOS_ERR_INVALID_FORMAT | posv;
+        else if (err == kPanic) sv = PACKOS_STATUS_PANIC | posv;
         else sv = (uint32_t)(d == 0 ? err : PACKOS_ERR_INVALID_FORMAT) | posv;
     }
     return sv;
@@ -1171,7 +1179,10 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECWIN_ATTR void k_decode_win(DecPro
         // the window when the tile holds the whole blob, or (per-blob windows)
         // when no fixed payload follows a var one (P.win > 0: the window is the
         // static prefix, which pass 1 confines every fixed payload to)
-        const bool inside = tile_mode ? (a0 >= b0 && a1 <= b0 + wbytes && a1 >= a0) : P.win > 0;
+        // (and only when that prefix, from the blob's offset in its first
+        // chunk, fits the WC chunks: a longer prefix was cut at b0 + 16 * WC)
+        const bool inside = tile_mode ? (a0 >= b0 && a1 <= b0 + wbytes && a1 >= a0)
+                                      : P.win > 0 && (a0 - b0) + (uint64_t)P.win <= 16ull * WC;
         if (inside) sv = decode_flat_k(FA, LReader{(const uint32_t*)w, b0, tile_mode ? 1u : (uint32_t)kBlock}, a0, a1, i);
         else sv = decode_flat_k(FA, R, a0, a1, i);
     } else if (P.flat) {
@@ -1283,7 +1294,9 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
         const DecChk c = F.vchk[e - j * (uint32_t)F.n_vchk];
         const uint32_t a = j * B + c.blob_off;
         bool bad;
-        if (c.flags & CHK_RANGE) {
+        if (c.flags & CHK_FAIL) {
+            bad = true;   // the container is present: its Encode fails whatever the value
+        } else if (c.flags & CHK_RANGE) {
             uint64_t u = 0;
             for (uint32_t b = 0; b < c.width; b++) u |= (uint64_t)lds_u8(lds, a + b) << (8 * b);
             const int sh = 64 - 8 * (int)c.width;
@@ -1568,13 +1581,14 @@ __global__ __launch_bounds__(kBlock) void k_get_field(const uint8_t* __restrict_
 #endif
     if (!out_values) return;
     uint8_t* dst = out_values + i * value_width;
-    if (value_width == 8 && ((uintptr_t)dst & 7) == 0) {
+    // a value wider than 8 B (big) is copied bytewise whatever value_width is
+    if (!big && value_width == 8 && ((uintptr_t)dst & 7) == 0) {
 #ifndef PACKOS_GET_PLAIN
         __builtin_nontemporal_store(val, (uint64_t*)dst);
 #else
         *(uint64_t*)dst = val;
 #endif
-    } else if (value_width == 4 && ((uintptr_t)dst & 3) == 0) {
+    } else if (!big && value_width == 4 && ((uintptr_t)dst & 3) == 0) {
         *(uint32_t*)dst = (uint32_t)val;
     } else if (!big) {
         for (uint32_t k = 0; k < value_width; k++) dst[k] = k < 8 ? (uint8_t)(val >> (8 * k)) : 0;
@@ -2081,6 +2095,9 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
     return PACKOS_OK;
 }
 
+static thread_local const char* g_last_encoder = "";
+const char* packos_last_encoder(void) { return g_last_encoder; }
+
 static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& ec, bool any_nil, size_t n,
                              uint8_t* out, uint64_t cap, uint64_t* out_offsets, uint32_t* status, void* ws,
                              size_t ws_bytes, uint32_t flags, hipStream_t st) {
@@ -2120,9 +2137,11 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
             pgen.fc_lds = (int32_t)gen_tables;
             const size_t lds_dw = (size_t)pdw.fc_lds + fcb;
             if (variant == 2) {
+                g_last_encoder = "fixed_dw";
                 hipLaunchKernelGGL(k_encode_fixed_dw, dim3((unsigned)tiles), dim3(kBlock), lds_dw, st, pdw, ec, out,
                                    (uint64_t)n, status, stv);
             } else if (variant == 13) {
+                g_last_encoder = "fixed_tile";
                 FixStage S;
                 memset(&S, 0, sizeof(S));
                 S.n = (int32_t)s->fcols.size();
@@ -2143,6 +2162,7 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
                                        out + b0 * B, rem, status ? status + b0 : nullptr, stv);
                 }
             } else {
+                g_last_encoder = "fixed";
                 hipLaunchKernelGGL(k_encode_fixed, dim3((unsigned)tiles), dim3(kBlock), gen_tables + fcb, st, pgen, ec,
                                    out, (uint64_t)n, status, stv);
             }
@@ -2153,6 +2173,7 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
         const size_t npos = s->items.size() + 1;
         const size_t lds = (size_t)kWavesPerBlock * (kSlot + ((npos * 4 + 15) / 16) * 16);
         const unsigned grid = (unsigned)std::min<uint64_t>((n + kWavesPerBlock - 1) / kWavesPerBlock, 256 * 16);
+        g_last_encoder = "var";
         hipLaunchKernelGGL(k_encode_var, dim3(grid), dim3(kBlock), lds, st, t->enc, ec, (const uint64_t*)nullptr, B,
                            out, cap, (uint64_t)n, status);
         HIP_TRY(hipGetLastError());
@@ -2173,6 +2194,7 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
         const size_t lds = (size_t)kWavesPerBlock * ext_pos_words((int)s->items.size()) * 4;
         if (lds > 64 * 1024) { set_error("schema has too many items for the LDS budget"); return PACKOS_E_UNSUPPORTED; }
         const unsigned grid = (unsigned)std::min<uint64_t>((n + kWavesPerBlock - 1) / kWavesPerBlock, 256 * 16);
+        g_last_encoder = "ext";
         hipLaunchKernelGGL(k_encode_ext, dim3(grid), dim3(kBlock), lds, st, t->enc, ec, (const uint64_t*)out_offsets,
                            (uint64_t)0, out, cap, (uint64_t)n, status);
         HIP_TRY(hipGetLastError());
@@ -2189,6 +2211,7 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
         FPlan F;
         if (flat_plan(s, ec, F)) {
             const dim3 g((unsigned)((n + kFT - 1) / kFT));
+            g_last_encoder = "flat";
 #define PACKOS_FLAT(NV) \
     hipLaunchKernelGGL((k_encode_flat<NV>), g, dim3(kFNT), F.lds_total, st, F, out_offsets, out, cap, (uint64_t)n, status)
             if (F.nvar <= 1) PACKOS_FLAT(1);
@@ -2214,6 +2237,7 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
             V.seg[V.oseg].r0 = V.seg[V.oseg].lds + (uint32_t)((uintptr_t)out_offsets & 15);
         }
         const uint64_t ntiles = (n + kVT - 1) / kVT;
+        g_last_encoder = "tiles";
 #ifdef PACKOS_PHASE_PROF
         unsigned long long* prof = nullptr;   // debug build only: per-tile phase clocks
         HIP_TRY(hipMalloc(&prof, ntiles * 8 * sizeof(unsigned long long)));
@@ -2262,6 +2286,7 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
     const size_t lds = (size_t)kWavesPerBlock * (kSlot + ((npos * 4 + 15) / 16) * 16);
     if (lds > 64 * 1024) { set_error("schema has too many items for the LDS budget"); return PACKOS_E_UNSUPPORTED; }
     const unsigned grid = (unsigned)std::min<uint64_t>((n + kWavesPerBlock - 1) / kWavesPerBlock, 256 * 16);
+    g_last_encoder = "var";
     hipLaunchKernelGGL(k_encode_var, dim3(grid), dim3(kBlock), lds, st, t->enc, ec, (const uint64_t*)out_offsets,
                        (uint64_t)0, out, cap, (uint64_t)n, status);
     HIP_TRY(hipGetLastError());

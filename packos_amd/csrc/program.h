@@ -22,6 +22,8 @@ enum : uint32_t {
     CHK_PREFIX = 8u,     // strings.HasPrefix(value, lit)   -> ErrStringPrefix
     CHK_SUFFIX = 16u,    // strings.HasSuffix(value, lit)   -> ErrStringSuffix
     CHK_DEFAULT = 32u,   // empty payload decodes as the default literal
+    CHK_FAIL = 64u,      // encode check only: fails whenever its container is present
+                         // (TupleSchemaNamed names / schemas length mismatch, schema.go:1808-1810)
     CHK_RANGE = CHK_MIN | CHK_MAX,
     CHK_STR = CHK_PREFIX | CHK_SUFFIX,
 };
@@ -177,6 +179,15 @@ struct FixStage {
 };
 
 // ---------------------------------------------------------------- decode ----
+// DecNode.variable flags of a tuple
+enum : uint8_t {
+    DT_VARIABLE = 1,    // VariableLength: no arg-count check
+    DT_NAMED = 2,       // TupleSchemaNamed: the arg-count check has no argCount > 0 guard
+                        // (schema.go:1773 vs TupleSchema's :1607)
+    DT_NAMES_BAD = 4,   // TupleSchemaNamed, len(FieldNames) != len(Schemas): Decode fails
+                        // first with ErrConstraintViolated at position 0 (schema.go:1756-1758)
+};
+
 struct DecNode {
     int32_t kind;      // NodeKind
     int32_t width;     // scalar width, or SchemaString/SchemaBytes Width
@@ -184,7 +195,7 @@ struct DecNode {
     int32_t nkids;
     int32_t kid0;      // first entry in the kid list
     uint8_t nullable;  // precheck nullable flag (schema IsNullable())
-    uint8_t variable;  // TupleSchema.VariableLength
+    uint8_t variable;  // tuples: DT_* flags
     uint8_t tag;
     uint8_t pad;
     uint32_t lit, lit_len;    // K_MATCH literal, or the Prefix / Suffix literal

@@ -17,6 +17,8 @@ struct Node {
     int width = 0;         // scalar width / SchemaString|SchemaBytes Width
     bool nullable = false; // scalar Nullable / TupleSchema.Nullable
     bool variable = false; // TupleSchema.VariableLength
+    bool named = false;    // TupleSchemaNamed (arg-count check without the argCount > 0 guard)
+    bool names_bad = false; // TupleSchemaNamed with len(FieldNames) != len(Schemas)
     bool sorted = false;   // map pairs sorted by key (PackMapSorted)
     std::string literal;   // K_MATCH
     // value checks (schema.go:1172-1364 Range, :2188-2250 SDateRange,

@@ -266,8 +266,13 @@ class Schema:
             return {"type": "bytes", "width": self.width} if self.width > 0 else {"type": "bytes"}
         if k == "tuple":
             d = {"type": "tuple", "schema": [c.to_json() for c in self.children]}
-            if self.names is not None:
+            if self.names:
                 d["fieldNames"] = list(self.names)
+            elif self.names is not None:
+                # STupleNamed(nil, ...): BuildSchema routes an empty fieldNames to
+                # STuple (schemabuilder_json.go:245), so the reference JSON cannot
+                # say "named"; this build's compiler reads the extra key
+                d["named"] = True
             if self.variable:
                 d["variableLength"] = True
             if self.flatten:
@@ -489,7 +494,8 @@ def BuildSchema(js) -> Schema:
         flat = var and bool(js.get("flatten", False))
         # every STuple* is Nullable: true; BuildSchema never reads the key
         node = Schema("tuple", nullable=True, children=tuple(kids),
-                      names=tuple(names) if names else None, variable=var, flatten=flat)
+                      names=tuple(names) if names else (() if js.get("named") else None),
+                      variable=var, flatten=flat)
         return node
     if t == "map":
         kids = [BuildSchema(c) for c in js.get("schema", [])]

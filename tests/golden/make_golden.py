@@ -100,8 +100,12 @@ def MAP(*kv, sorted_=False):
 
 def TUP(*kids, names=None):
     d = {"type": "tuple", "schema": list(kids)}
-    if names is not None:
+    if names:
         d["fieldNames"] = names
+    elif names is not None:
+        # STupleNamed(nil, ...): BuildSchema routes an empty fieldNames to STuple
+        # (schemabuilder_json.go:245), so this build marks the named form itself
+        d["named"] = True
     return d
 
 
@@ -204,6 +208,12 @@ INPUTS = [
      [S("2025-09-10"), 42, S("alice@example.com"), S("prefix-hello"), S("world-suffix")]),
     ("pack_defaults_empty", "schema/schema_test.go:443-450 (pack.Pack with three empty strings)", "packable",
      [STR, I32, STR, STR, STR], [S("2025-09-10"), 42, S(""), S(""), S("")]),
+    ("pack_four_tuples", "schema/schema_test.go:559-583 (pack.Pack of four tuples)", "packable",
+     [TUP(I32, BOOL, STR), TUP(I16, BOOL, STR), TUP(I32, BOOL, STR), TUP(I32, BOOL, STR)],
+     [[2025, False, S("az")], [7, True, S("go")], [111, True, S("xx")], [222, False, S("yy")]]),
+    # derived: pack.Pack(pack.PackTuple(pack.PackInt16(7))) = 24 00 30 00 21 00 10 00 07 00
+    ("pack_one_tuple_int16", "derived: pack.Pack(pack.PackTuple(pack.PackInt16(7)))", "packable",
+     [TUP(I16)], [[7]]),
 ]
 
 PACKED_MAP = MAP(EX("meta"), MAP(EX("role"), {"type": "bytes", "width": 5}, EX("user"), {"type": "bytes", "width": 5}),
@@ -257,6 +267,29 @@ DECODE = [
     ("decode_two_tuples", "schema/schema_test.go:363-404", "pack_two_tuples34",
      [TUP(I32, BOOL, {"type": "string", "width": 2}), TUP(I16, BOOL, {"type": "string", "width": 2})],
      [[2025, False, S("az")], [7, True, S("go")]], 0),
+    ("decode_named_tuples", "schema/schema_test.go:478-531 (DecodeBufferNamed)", "pack_two_tuples34",
+     {"type": "chain", "fieldNames": ["firstTuple", "secondTuple"], "schema": [
+         TUP(I32, BOOL, {"type": "string", "width": 2}, names=["year", "flag", "code"]),
+         TUP(I16, BOOL, {"type": "string", "width": 2}, names=["num", "flag", "lang"])]},
+     {"firstTuple": {"year": 2025, "flag": False, "code": S("az")},
+      "secondTuple": {"num": 7, "flag": True, "lang": S("go")}}, 0),
+    ("decode_extra_tuples_ignored", "schema/schema_test.go:559-610", "pack_four_tuples",
+     [TUP(I32, BOOL, {"type": "string", "width": 2}), TUP(I16, BOOL, {"type": "string", "width": 2})],
+     [[2025, False, S("az")], [7, True, S("go")]], 0),
+    # derived (schema.go:1607): STuple() with no schemas skips the arg-count
+    # check (argCount > 0 guard), so a 1-field tuple decodes as an empty one
+    ("derived_unnamed_empty_tuple_any_count", "derived: schema/schema.go:1604-1609", "pack_one_tuple_int16",
+     [TUP()], [[]], 0),
+    # derived (schema.go:1773-1775): STupleNamed(nil) has no such guard:
+    # 1 field != 0 schemas -> ErrConstraintViolated at position 0
+    ("derived_named_nil_tuple_count", "derived: schema/schema.go:1766-1775", "pack_one_tuple_int16",
+     [TUP(names=[])], None, (3 | (1 << 8))),
+    # derived (schema.go:1756-1758): a named tuple whose FieldNames and
+    # Schemas differ in length fails before precheck, at position 0 even as
+    # the second field of the chain
+    ("derived_named_names_mismatch", "derived: schema/schema.go:1756-1758", "pack_two_tuples34",
+     [TUP(I32, BOOL, {"type": "string", "width": 2}),
+      TUP(I16, BOOL, {"type": "string", "width": 2}, names=["num", "flag"])], None, (3 | (1 << 8))),
     ("decode_empty_tuples2", "schema/schema_test.go:840-869", "schema_empty_tuples2",
      [I16, TUP(STR, STR, STR), TUP(), TUP(STR, names=["ok"]), TUP(names=[]), I16],
      [5, None, None, None, None, 5], 0),

@@ -138,7 +138,9 @@ class OracleSchema:
                 nodes.extend([7, len(lits), n.width, 0])
                 lits.append(n.literal)
             elif k == "tuple":
-                nodes.extend([8, int(n.nullable), len(n.children), int(n.variable)])
+                named = n.names is not None
+                bad = named and len(n.names) != len(n.children)
+                nodes.extend([8, int(n.nullable), len(n.children), int(n.variable) | 2 * named | 4 * bad])
             elif k == "map":
                 nodes.extend([9, int(n.sorted), len(n.children), 0])
             else:

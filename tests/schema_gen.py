@@ -30,7 +30,10 @@ def rand_node(rng, depth, allow_var=True, allow_null=True):
         k = rng.randint(0, 4)
         kids = [rand_node(rng, depth + 1, allow_var, allow_null) for _ in range(k)]
         if rng.random() < 0.3:
-            return STupleNamed([f"f{j}" for j in range(k)], *kids)
+            # STupleNamed(nil) for empty tuples half the time: its arg-count
+            # check has no argCount > 0 guard (schema.go:1773)
+            names = None if k == 0 and rng.random() < 0.5 else [f"f{j}" for j in range(k)]
+            return STupleNamed(names, *kids)
         return STuple(*kids)
     if depth < 3 and r < 0.27:
         k = rng.randint(0, 3)
@@ -119,6 +122,13 @@ def rand_checked_node(rng, depth, allow_var=True, allow_null=True):
     r = rng.random()
     if depth < 2 and r < 0.15:
         kids = [rand_checked_node(rng, depth + 1, allow_var, allow_null) for _ in range(rng.randint(1, 3))]
+        r2 = rng.random()
+        if r2 < 0.1:
+            # FieldNames shorter than Schemas: Encode of a present value and every
+            # Decode fail with ErrConstraintViolated (schema.go:1756-1758, 1808-1810)
+            return STupleNamed([f"f{j}" for j in range(len(kids) - 1)], *kids)
+        if r2 < 0.3:
+            return STupleNamed([f"f{j}" for j in range(len(kids))], *kids)
         return STuple(*kids)
     if depth < 2 and r < 0.25:
         keys = rng.sample(["alpha", "beta", "gamma", "zz"], rng.randint(1, 2))

@@ -18,8 +18,10 @@ from packos_amd.schema import (SBool, SBytes, SChain, SInt16, SInt32, SInt64, SS
 
 pytestmark = pytest.mark.gpu
 
+# fixed leaves of at most 16 B (k_encode_flat stages them; longer ones send the
+# chain to k_encode_tiles)
 LEAVES = [lambda: SBool, lambda: SUint8, lambda: SInt16, lambda: SInt32, lambda: SInt64, lambda: SStringLen(5),
-          lambda: SBytes(17), lambda: SStringLen(40)]
+          lambda: SBytes(13), lambda: SStringLen(16)]
 LENS = [0, 1, 3, 7, 15, 16, 17, 31, 33, 80, 255, 1000, 4000]
 
 
@@ -32,13 +34,18 @@ def flat_chain(rng):
     k = rng.randint(1, 12)
     leaves, nvar = [], 0
     for _ in range(k):
-        if rng.random() < 0.4 and nvar < 8:
+        if rng.random() < 0.4 and nvar < 4:   # k_encode_flat takes <= 4 var leaves
             leaves.append(SVariableString() if rng.random() < 0.5 else SVariableBytes())
             nvar += 1
         else:
             leaves.append(rng.choice(LEAVES)())
     if nvar == 0:
         leaves.insert(rng.randint(0, len(leaves)), SVariableBytes())
+    # >= 15 static bytes before the first var value (flat_plan's condition):
+    # header words of the leading fixed leaves + their widths, else an SInt64 lead
+    nlead = next(j for j, x in enumerate(leaves) if x.width <= 0 and x.kind in ("string", "bytes"))
+    if 2 * (len(leaves) + 1) + sum(x.width for x in leaves[:nlead]) < 15:
+        leaves.insert(0, SInt64)
     return SChain(*leaves)
 
 
@@ -59,7 +66,7 @@ def rows(chain, n, seed, lens=LENS):
     return [[value(rng, s, lens) for s in chain.Schemas] for _ in range(n)]
 
 
-def check(chain, hc, mode, what, shift=False, off64=False):
+def check(chain, hc, mode, what, shift=False, off64=False, kernel="flat"):
     T = torch()
     s = CompiledSchema(chain, mode)
     dc = DeviceColumns.from_host(s, hc, "cuda:0")
@@ -86,6 +93,8 @@ def check(chain, hc, mode, what, shift=False, off64=False):
     assert L.packos_encode_batch(s.handle, arr, n, out.data_ptr(), out.numel(), offs.data_ptr(), st.data_ptr(),
                                  None, 0, 0, None) == 0, L.packos_last_error()
     T.cuda.synchronize()
+    if kernel:   # the encoder under test actually ran (not a silent fallback)
+        assert L.packos_last_encoder().decode() == kernel, (what, L.packos_last_encoder())
     o1 = offs.cpu().numpy().astype(np.uint64)
     assert np.array_equal(o1, o0), f"{what}: offsets differ"
     a1 = out[: int(o0[n])].cpu().numpy()
@@ -110,11 +119,20 @@ def test_flat_random_flat(seed):
     check(chain, hc, seed % 2, f"seed {seed}", shift=seed % 3 == 1, off64=seed % 4 == 3)
 
 
+def test_flat_wide_fixed_leaf_falls_back():
+    """A fixed leaf over 16 B is outside k_encode_flat's plan: the tile
+    encoder takes the chain, bit-exact."""
+    chain = SChain(SInt64, SVariableString(), SStringLen(40), SBytes(17))
+    hc = HostColumns.from_rows(chain, rows(chain, 700, 3))
+    check(chain, hc, 0, "wide fixed", kernel="tiles")
+
+
 @pytest.mark.parametrize("lens", [[0], [0, 1], [16], [4000, 0], [7000, 9000]], ids=str)
 def test_flat_length_regimes(lens):
     """All-empty values, 16-B values, multi-page values and blobs past the
     13-bit header range (status PACKOS_STATUS_OVERFLOW13)."""
-    chain = SChain(SInt16, SVariableString(), SInt64, SVariableBytes(), SBool)
+    # SInt64 first: >= 15 static bytes ahead of the first var value (flat_plan)
+    chain = SChain(SInt64, SInt16, SVariableString(), SInt64, SVariableBytes(), SBool)
     hc = HostColumns.from_rows(chain, rows(chain, 600, 99, lens))
     check(chain, hc, 0, f"lens {lens}")
 
@@ -128,7 +146,7 @@ def test_flat_configs(name, n, flat, monkeypatch):
     cfg = CONFIGS[name]
     hc = make_columns(cfg, n=n)
     for mode in (0, 1):
-        check(cfg.chain, hc, mode, f"{name} flat={flat} mode {mode}")
+        check(cfg.chain, hc, mode, f"{name} flat={flat} mode {mode}", kernel="flat" if flat == "1" else "tiles")
 
 
 def test_flat_capacity_overrun():

@@ -5,6 +5,7 @@ the oracle on the same seeded inputs (oracle pinned by test_oracle_golden.py)
 or with the reference's golden bytes directly.
 """
 import ctypes as C
+import random
 
 import numpy as np
 import pytest
@@ -522,6 +523,23 @@ def test_random_decode_roundtrip(seed):
         assert (st == 0).all()
 
 
+@pytest.mark.parametrize("k,w", [(6, 8), (12, 8), (15, 8), (15, 4), (13, 8)])
+def test_decode_long_static_prefix(k, w):
+    """A flat chain whose static prefix (header block + k fixed fields) is
+    longer than the decoder's per-blob LDS window, then a trailing var field:
+    blobs large enough for per-blob windows, at unaligned arena offsets.  The
+    flat fast path must not read the prefix's tail from the (short) window."""
+    leaf = SInt64 if w == 8 else SInt32
+    chain = SChain(*([leaf] * k), SVariableString())
+    rng = random.Random(k * 31 + w)
+    rows = [[rng.getrandbits(8 * w) for _ in range(k)] +
+            ["".join(chr(rng.randint(0x20, 0x7E)) for _ in range(rng.randint(0, 300)))] for _ in range(3000)]
+    hc = HostColumns.from_rows(chain, rows)
+    arena, offs, _ = ob.encode(chain, hc, 0)
+    st = assert_same_decode(chain, arena, offs, hc.n, f"k={k} w={w}")
+    assert (st == 0).all()
+
+
 @pytest.mark.parametrize("seed", range(40))
 def test_random_decode_corrupted(seed):
     # flip header bytes / truncate blobs: every error code, position and panic
@@ -888,6 +906,31 @@ def test_get_batch_nullable_and_any_width():
         assert np.array_equal(o[4], g[4].cpu().numpy())
         if o[0] is not None:
             assert np.array_equal(o[0], g[0].cpu().numpy())
+
+
+@pytest.mark.parametrize("vw", [4, 8, 16, 24])
+def test_get_batch_wide_value_narrow_buffer(vw):
+    """A 16-B FIXED value gathered into rows of value_width bytes: the first
+    min(16, vw) payload bytes, zero-padded (never the 8-B register path)."""
+    T = torch()
+    chain = SChain(SInt16, SStringLen(16))
+    rows = [[i, "".join(chr(0x41 + (i + k) % 26) for k in range(16))] for i in range(300)]
+    hc = HostColumns.from_rows(chain, rows)
+    arena, offs, _ = ob.encode(chain, hc, 0)
+    da = T.from_numpy(arena).to("cuda:0")
+    n = hc.n
+    vals = T.zeros((n, vw), dtype=T.uint8, device="cuda:0")
+    st = T.zeros(n, dtype=T.uint8, device="cuda:0")
+    p = (C.c_int32 * 1)(1)
+    B = int(offs[1])
+    assert _lib.lib().packos_get_batch(da.data_ptr(), None, B, n, p, 1, 0, 6, 16, vals.data_ptr(), vw,
+                                       None, None, None, st.data_ptr(), None) == 0
+    T.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    got = vals.cpu().numpy()
+    for i in range(n):
+        want = rows[i][1].encode()[:vw].ljust(vw, b"\0")
+        assert bytes(got[i]) == want, i
 
 
 def _rand_map_value(rng, depth):
