@@ -219,6 +219,46 @@ def shard_parity(cfg, hc, gpu_arena, gpu_offsets, threads, max_blobs=1 << 21):
     return same, hashlib.sha256(gpu_arena[:total].tobytes()).hexdigest()[:16]
 
 
+def decode_parity(cfg, arena, offsets, stride, n, gout, gst, threads):
+    """Whole-shard check of a timed decode: the CPU oracle's DecodeBuffer of
+    the same arena must give the same status word for every blob and the same
+    columns (fixed values, validity, views) for every blob that decodes."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bridge as ob  # checker only
+    o_out, o_st = ob.decode(cfg.chain, arena, offsets, n, stride=stride, nthreads=threads)
+    g_st = gst[:n].cpu().numpy().astype(np.uint32)
+    same = bool(np.array_equal(o_st[:n], g_st))
+    ok = o_st[:n] == 0
+    h = hashlib.sha256(g_st.tobytes())
+    for c, sp in enumerate(o_out.specs):
+        for name in ("data", "valid", "start", "length"):
+            a = getattr(o_out, name)[c]
+            if a is None or not same:
+                continue
+            b = getattr(gout, name)[c].cpu().numpy()
+            b = b.view(np.uint64) if name == "start" else b.view(np.uint32) if name == "length" else b
+            if name == "data":
+                a2, b2 = a[: n * sp.width].reshape(n, sp.width), b[: n * sp.width].reshape(n, sp.width)
+                same = same and bool(np.array_equal(a2[ok], b2[ok]))
+            else:
+                same = same and bool(np.array_equal(a[:n][ok], b[:n][ok]))
+            h.update(np.ascontiguousarray(b[: n * (sp.width if name == "data" else 1)]).tobytes())
+    return same, int(ok.sum()), h.hexdigest()[:16]
+
+
+def get_parity(arena, offsets, stride, n, path, getter, gvals, gst):
+    """Whole-shard check of a timed GetAccess gather against the CPU oracle's
+    getter: status for every blob, the typed value for every blob it returns."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bridge as ob  # checker only
+    o_vals, _, _, _, o_st = ob.get_batch(arena, offsets, n, path, getter, stride=stride)
+    g_st = gst[:n].cpu().numpy()
+    g_vals = gvals[:n].cpu().numpy()
+    ok = o_st[:n] == 0
+    same = bool(np.array_equal(o_st[:n], g_st)) and bool(np.array_equal(o_vals[:n][ok], g_vals[ok]))
+    return same, int(ok.sum()), hashlib.sha256(g_vals.tobytes() + g_st.tobytes()).hexdigest()[:16]
+
+
 def pcie_ceiling(dev, nbytes=256 << 20, reps=4, piece=64 << 20):
     """Pinned host <-> device copy rates of this box (GB/s) with plain HIP
     calls (libamdhip64 through ctypes): H2D alone, D2H alone, and both at once
@@ -415,9 +455,12 @@ def main():
             p.run()
         torch.cuda.synchronize()
 
+        outs = []
+
         def dec_runner(p):
             dcols = DecodedColumns(schema, n, dev)
             st = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+            outs.append((dcols, st))
             if fixed:
                 return lambda: decode_batch(schema, p.out, None, n, stride=p.B, stream=stream, out=dcols, status=st)
             return lambda: decode_batch(schema, p.out, p.offsets, n, stream=stream, out=dcols, status=st)
@@ -441,9 +484,11 @@ def main():
             stride = p.B if fixed else 0
             sp = C.c_void_p(stream.cuda_stream)
             s0, ln, tg = (t.data_ptr() for t in sps) if args.get_spans else (None, None, None)
+            outs.append((vals, st))
             return lambda: L.packos_get_batch(p.out.data_ptr(), offs, stride, n, path, 1, _lib_get_int, 0, 0,
                                               vals.data_ptr(), 8, s0, ln, tg, st.data_ptr(), sp)
         _lib_get_int = 3   # PACKOS_GET_INT
+        outs = []
         runs = [get_runner(p) for p in sets]
 
     def timed(plans, steps, warmup):
@@ -516,7 +561,7 @@ def main():
     # its provenance, is read from profiles/ when present.
     traffic, traffic_src = None, None
     pmc_name = f"pmc_{args.config}.json" if args.op == "encode" else f"pmc_{args.config}_{args.op}.json"
-    for rnd in ("r03", "r02"):
+    for rnd in ("r04", "r03", "r02"):
         pmc_path = os.path.join(ROOT, "profiles", rnd, pmc_name)
         if not os.path.exists(pmc_path):
             continue
@@ -564,6 +609,30 @@ def main():
                   "blobs_rank0": n, "checked_blobs_per_rank": min(n, 1 << 21), "sha256_16_rank0": digest,
                   "checked": "every rank: its GPU shard (its first 2M blobs when larger) vs the CPU oracle's "
                              "encoding of the same global slice"}
+    if args.op != "encode" and os.environ.get("PACKOS_BENCH_NO_PARITY") is None:
+        # the timed run's set-0 outputs vs the CPU oracle over this rank's whole
+        # shard (every rank; flags meet in a MIN)
+        arena_np = sets[0].out[:total_out].cpu().numpy()
+        offs_np = None if fixed else sets[0].offsets.cpu().numpy().astype(np.uint64)
+        stride = schema.fixed_blob_size if fixed else 0
+        hi_ = host_info()
+        th = max(1, (int(hi_["cgroup_cpu_quota"] or 0) or hi_["affinity"] or 1) // max(1, int(
+            os.environ.get("LOCAL_WORLD_SIZE", world))))
+        if args.op == "decode":
+            same, n_ok, digest = decode_parity(cfg, arena_np, offs_np, stride, n, outs[0][0], outs[0][1], th)
+            what = "status of every blob + columns / validity / views of every blob that decodes"
+        else:
+            same, n_ok, digest = get_parity(arena_np, offs_np, stride, n, [args.get_pos], 3, outs[0][0], outs[0][1])
+            what = "status of every blob + GetInt value of every blob that has one"
+        del arena_np
+        if world > 1:
+            flag = torch.tensor([1 if same else 0], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            same = int(flag.item()) == 1
+        parity = {"result": "bit-exact" if same else "MISMATCH", "ranks": world, "blobs": n, "blobs_ok": n_ok,
+                  "sha256_16": digest,
+                  "checked": f"GPU {args.op} outputs of the timed run (set 0) vs the CPU oracle over the whole "
+                             f"shard{' of every rank' if world > 1 else ''}: {what}"}
     if rank == 0 and world == 1 and not args.no_host:
         try:
             host = host_leg(schema, make_columns(cfg, n=min(n, 1 << 22), lo=lo), dev)

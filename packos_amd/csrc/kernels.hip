@@ -2209,14 +2209,20 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
     const bool flat_ok = s->tune.enc_flat == 1 || (s->tune.enc_flat == 2 && n && cap / n >= kFlatMinBlob);
     if (flat_ok && !offs_ready && !(flags & PACKOS_ENC_FORCE_GENERIC) && affine_layout(s, ec, nullptr)) {
         FPlan F;
-        if (flat_plan(s, ec, F)) {
+        if (flat_plan(s, ec, F, (uint32_t)s->tune.flat_w)) {
             const dim3 g((unsigned)((n + kFT - 1) / kFT));
-            g_last_encoder = "flat";
-#define PACKOS_FLAT(NV) \
-    hipLaunchKernelGGL((k_encode_flat<NV>), g, dim3(kFNT), F.lds_total, st, F, out_offsets, out, cap, (uint64_t)n, status)
-            if (F.nvar <= 1) PACKOS_FLAT(1);
-            else if (F.nvar <= 2) PACKOS_FLAT(2);
-            else PACKOS_FLAT(4);
+            g_last_encoder = F.wbytes ? "flat_s" : "flat";
+#define PACKOS_FLAT(K, NV) \
+    hipLaunchKernelGGL((K<NV>), g, dim3(kFNT), F.lds_total, st, F, out_offsets, out, cap, (uint64_t)n, status)
+            if (F.wbytes) {
+                if (F.nvar <= 1) PACKOS_FLAT(k_encode_flat_s, 1);
+                else if (F.nvar <= 2) PACKOS_FLAT(k_encode_flat_s, 2);
+                else PACKOS_FLAT(k_encode_flat_s, 4);
+            } else {
+                if (F.nvar <= 1) PACKOS_FLAT(k_encode_flat, 1);
+                else if (F.nvar <= 2) PACKOS_FLAT(k_encode_flat, 2);
+                else PACKOS_FLAT(k_encode_flat, 4);
+            }
 #undef PACKOS_FLAT
             HIP_TRY(hipGetLastError());
             return PACKOS_OK;

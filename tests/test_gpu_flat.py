@@ -66,7 +66,7 @@ def rows(chain, n, seed, lens=LENS):
     return [[value(rng, s, lens) for s in chain.Schemas] for _ in range(n)]
 
 
-def check(chain, hc, mode, what, shift=False, off64=False, kernel="flat"):
+def check(chain, hc, mode, what, shift=False, off64=False, kernel=None):
     T = torch()
     s = CompiledSchema(chain, mode)
     dc = DeviceColumns.from_host(s, hc, "cuda:0")
@@ -105,18 +105,26 @@ def check(chain, hc, mode, what, shift=False, off64=False, kernel="flat"):
     assert np.array_equal(st.cpu().numpy().astype(np.uint32), s0), f"{what}: status differs"
 
 
-@pytest.fixture(autouse=True)
-def flat_on(monkeypatch):
+# PACKOS_FLAT_W: the streaming kernel's window bytes (default 12288; 64 cuts
+# nearly every blob across windows), 0 = the chunk-gather kernel
+FLAT_W = ["12288", "0", "64"]
+FLAT_NAME = {"0": "flat"}
+
+
+@pytest.fixture(autouse=True, params=FLAT_W, ids=lambda w: f"W{w}")
+def flat_on(request, monkeypatch):
     monkeypatch.setenv("PACKOS_ENC_FLAT", "1")   # read when the schema compiles
+    monkeypatch.setenv("PACKOS_FLAT_W", request.param)
+    return FLAT_NAME.get(request.param, "flat_s")
 
 
 @pytest.mark.parametrize("seed", range(40))
-def test_flat_random_flat(seed):
+def test_flat_random_flat(seed, flat_on):
     rng = random.Random(seed)
     chain = flat_chain(rng)
     n = [1, 127, 128, 129, 300, 1000, 2049][seed % 7]
     hc = HostColumns.from_rows(chain, rows(chain, n, seed * 11 + 5))
-    check(chain, hc, seed % 2, f"seed {seed}", shift=seed % 3 == 1, off64=seed % 4 == 3)
+    check(chain, hc, seed % 2, f"seed {seed}", shift=seed % 3 == 1, off64=seed % 4 == 3, kernel=flat_on)
 
 
 def test_flat_wide_fixed_leaf_falls_back():
@@ -128,25 +136,25 @@ def test_flat_wide_fixed_leaf_falls_back():
 
 
 @pytest.mark.parametrize("lens", [[0], [0, 1], [16], [4000, 0], [7000, 9000]], ids=str)
-def test_flat_length_regimes(lens):
+def test_flat_length_regimes(lens, flat_on):
     """All-empty values, 16-B values, multi-page values and blobs past the
     13-bit header range (status PACKOS_STATUS_OVERFLOW13)."""
     # SInt64 first: >= 15 static bytes ahead of the first var value (flat_plan)
     chain = SChain(SInt64, SInt16, SVariableString(), SInt64, SVariableBytes(), SBool)
     hc = HostColumns.from_rows(chain, rows(chain, 600, 99, lens))
-    check(chain, hc, 0, f"lens {lens}")
+    check(chain, hc, 0, f"lens {lens}", kernel=flat_on)
 
 
 @pytest.mark.parametrize("flat", ["1", "0"])
 @pytest.mark.parametrize("name,n", [("C3", 20000), ("C5", 5000)])
-def test_flat_configs(name, n, flat, monkeypatch):
+def test_flat_configs(name, n, flat, monkeypatch, flat_on):
     """The configs through k_encode_flat and (PACKOS_ENC_FLAT=0) through
     k_encode_tiles, both modes."""
     monkeypatch.setenv("PACKOS_ENC_FLAT", flat)
     cfg = CONFIGS[name]
     hc = make_columns(cfg, n=n)
     for mode in (0, 1):
-        check(cfg.chain, hc, mode, f"{name} flat={flat} mode {mode}", kernel="flat" if flat == "1" else "tiles")
+        check(cfg.chain, hc, mode, f"{name} flat={flat} mode {mode}", kernel=flat_on if flat == "1" else "tiles")
 
 
 def test_flat_capacity_overrun():
