@@ -197,3 +197,16 @@ def test_get_batch_span_outputs_optional_only_for_typed_gathers():
     assert call(GET_SPAN, None, False) == -1
     assert call(GET_ANY, None, False) == -1
     assert call(GET_INT, None, False) == -1
+
+
+def test_json_marshal_shaped_schema_compiles():
+    """The text Go's json.Marshal makes of []schema.SchemaJSON
+    (schemabuilder_json.go:8-30): omitempty keys absent, "extra" holding any
+    JSON (objects, arrays, null, floats) that BuildSchema never reads.  Same
+    columns and layout as the bare schema."""
+    extra = {"label": "id", "order": 1, "tags": ["a", "b"], "ui": {"step": 0.5, "hidden": False, "hint": None}}
+    marshalled = json.dumps([{"type": "int16", "extra": extra}, {"type": "bool"}, {"type": "string"},
+                             {"type": "bytes", "extra": {}}], separators=(",", ":"))
+    bare = json.dumps([{"type": "int16"}, {"type": "bool"}, {"type": "string"}, {"type": "bytes"}])
+    a, b = CompiledSchema(marshalled), CompiledSchema(bare)
+    assert a.describe() == b.describe()
