@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <numeric>
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -1229,10 +1230,14 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
     uint32_t* lds = (uint32_t*)lds_raw;
     const uint32_t B = (uint32_t)F.B, T = (uint32_t)F.T, QW = (B + 3) >> 2;
+    // staged row stride: B, or B + 16 (F.pad) so that rows whose stride is a
+    // multiple of 128 B do not all start on one LDS bank (column reads gather
+    // one dword per row: 16-way conflicts for M's 256-B rows)
+    const uint32_t SB = B + (uint32_t)F.pad;
     const uint64_t blob0 = (uint64_t)blockIdx.x * T;
     const uint32_t rows = (uint32_t)min((uint64_t)T, n - blob0);
     const int tid = threadIdx.x;
-    uint32_t* chk = lds + (T * B / 4 + 4);
+    uint32_t* chk = lds + (T * SB / 4 + 4);
     uint32_t* fail = chk + 3 * QW;
 
     // the tile base is one scalar load; whether the tile's blobs really lie
@@ -1257,9 +1262,22 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
         const uint8_t* src = arena + base;
         const uint32_t n16 = bytes >> 4, lane = tid & 63, c00 = tid & ~63u;
         const uint32_t lds0 = (uint32_t)(uintptr_t)lds_raw;
-        for (uint32_t c0 = c00; c0 < n16; c0 += kBlock)
-            if (c0 + lane < n16) dma16(src + 16u * (c0 + lane), __builtin_amdgcn_readfirstlane(lds0 + 16u * c0));
-        for (uint32_t k = n16 * 16 + tid; k < bytes; k += kBlock) lds_raw[k] = src[k];
+        if (F.pad == 0) {
+            for (uint32_t c0 = c00; c0 < n16; c0 += kBlock)
+                if (c0 + lane < n16) dma16(src + 16u * (c0 + lane), __builtin_amdgcn_readfirstlane(lds0 + 16u * c0));
+            for (uint32_t k = n16 * 16 + tid; k < bytes; k += kBlock) lds_raw[k] = src[k];
+        } else {
+            // padded rows: LDS chunk L (written by lane L % 64 of a full-width
+            // DMA instruction) holds chunk c = L % cpr of row j = L / cpr, the
+            // global chunk j * cpb + c; the pad chunk (c == cpb) is not loaded
+            const uint32_t cpr = SB >> 4, cpb = B >> 4, NL = (n16 / cpb + 1) * cpr;
+            for (uint32_t c0 = c00; c0 < NL; c0 += kBlock) {
+                const uint32_t L = c0 + lane, j = __umulhi(L, (uint32_t)F.b_magic), c = L - j * cpr;
+                const uint32_t g = j * cpb + c;
+                if (c < cpb && g < n16) dma16(src + 16u * g, __builtin_amdgcn_readfirstlane(lds0 + 16u * c0));
+            }
+            for (uint32_t k = n16 * 16 + tid; k < bytes; k += kBlock) lds_raw[(k / B) * SB + k % B] = src[k];
+        }
     }
     if (offs) {
         for (uint32_t j = tid; j <= rows; j += kBlock) ok &= offs[blob0 + j] == base + (uint64_t)j * B;
@@ -1282,7 +1300,7 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
         for (uint32_t e = tid; e < rows * nq; e += kBlock) {
             const uint32_t j = nq > 1 ? __umulhi(e, nq_magic) : e;
             const uint32_t* c = chk + 3 * (e - j * nq);
-            const uint32_t a = j * B + 4 * c[0];   // blob dword q (B % 4 == 0: aligned)
+            const uint32_t a = j * SB + 4 * c[0];   // blob dword q (B % 4 == 0: aligned)
             const uint32_t v = (B & 3) == 0 ? lds[a >> 2] : lds_bytes4(lds, a);
             if ((v & c[1]) != c[2]) fail[j] = 1;
         }
@@ -1292,11 +1310,9 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
     for (uint32_t e = tid; e < rows * (uint32_t)F.n_vchk; e += kBlock) {
         const uint32_t j = e / (uint32_t)F.n_vchk;
         const DecChk c = F.vchk[e - j * (uint32_t)F.n_vchk];
-        const uint32_t a = j * B + c.blob_off;
+        const uint32_t a = j * SB + c.blob_off;
         bool bad;
-        if (c.flags & CHK_FAIL) {
-            bad = true;   // the container is present: its Encode fails whatever the value
-        } else if (c.flags & CHK_RANGE) {
+        if (c.flags & CHK_RANGE) {
             uint64_t u = 0;
             for (uint32_t b = 0; b < c.width; b++) u |= (uint64_t)lds_u8(lds, a + b) << (8 * b);
             const int sh = 64 - 8 * (int)c.width;
@@ -1319,13 +1335,13 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
             for (uint32_t d = tid; d < D; d += kBlock) {
                 const uint32_t b = 4 * d;
                 const uint32_t j = __umulhi(b, L.magic);
-                const uint32_t a = j * B + L.blob_off + (b - j * w);
+                const uint32_t a = j * SB + L.blob_off + (b - j * w);
                 __builtin_nontemporal_store(lds_bytes4(lds, a), dst + d);
             }
         } else if (w == 2) {   // a dword = rows 2d, 2d+1
             for (uint32_t d = tid; d < D; d += kBlock) {
-                const uint32_t a = 2 * d * B + L.blob_off;
-                const uint32_t x = (lds_bytes4(lds, a) & 0xFFFFu) | (lds_bytes4(lds, a + B) << 16);
+                const uint32_t a = 2 * d * SB + L.blob_off;
+                const uint32_t x = (lds_bytes4(lds, a) & 0xFFFFu) | (lds_bytes4(lds, a + SB) << 16);
                 __builtin_nontemporal_store(x, dst + d);
             }
         } else if (w > 4 && !(L.flags & 1u)) {   // most dwords sit inside one row
@@ -1335,11 +1351,11 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
                 const uint32_t r = b - j * w;
                 uint32_t x;
                 if (r + 4 <= w) {
-                    x = lds_bytes4(lds, j * B + L.blob_off + r);
+                    x = lds_bytes4(lds, j * SB + L.blob_off + r);
                 } else {
                     const uint32_t k = w - r;   // 1..3 bytes of row j, then row j + 1
-                    x = (lds_bytes4(lds, j * B + L.blob_off + r) & ((1u << (8 * k)) - 1u)) |
-                        (lds_bytes4(lds, (j + 1) * B + L.blob_off) << (8 * k));
+                    x = (lds_bytes4(lds, j * SB + L.blob_off + r) & ((1u << (8 * k)) - 1u)) |
+                        (lds_bytes4(lds, (j + 1) * SB + L.blob_off) << (8 * k));
                 }
                 __builtin_nontemporal_store(x, dst + d);
             }
@@ -1350,7 +1366,7 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
                 for (int y = 0; y < 4; y++) {
                     const uint32_t b = 4 * d + y;
                     const uint32_t j = w > 1 ? __umulhi(b, L.magic) : b;
-                    uint32_t v = lds_u8(lds, j * B + L.blob_off + (b - j * w));
+                    uint32_t v = lds_u8(lds, j * SB + L.blob_off + (b - j * w));
                     if (L.flags & 1u) v = v != 0;
                     x |= v << (8 * y);
                 }
@@ -1360,7 +1376,7 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
         // ragged tail (R % 4 bytes, last tile only)
         for (uint32_t b = 4 * D + tid; b < R; b += kBlock) {
             const uint32_t j = w > 1 ? __umulhi(b, L.magic) : b;
-            uint32_t v = lds_u8(lds, j * B + L.blob_off + (b - j * w));
+            uint32_t v = lds_u8(lds, j * SB + L.blob_off + (b - j * w));
             if (L.flags & 1u) v = v != 0;
             L.dst[blob0 * w + b] = (uint8_t)v;
         }
@@ -2342,9 +2358,17 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
         // small blobs the larger tile loses more to fewer workgroups (C2 +7 %)
         int64_t tb = B >= 128 ? kDecTileBytesLarge : kDecTileBytes;
         if (s->tune.dec_tile_bytes) tb = s->tune.dec_tile_bytes;
-        F.T = (int32_t)std::min<int64_t>(1024, std::max<int64_t>(16, (tb / B) / 16 * 16));
+        // staged rows padded by 16 B when the row stride would put every row's
+        // dword k on few LDS banks (dword reads bank on (a/4) % 32)
+        int pad = s->tune.dec_pad;
+        if (pad < 0) pad = (B % 16 == 0 && std::gcd<int64_t>(B / 4, 32) >= 8) ? 16 : 0;
+        if (B % 16) pad = 0;
+        F.pad = pad;
+        const int64_t SB = B + pad;
+        F.b_magic = pad ? (uint32_t)(((1ull << 32) + SB / 16 - 1) / (SB / 16)) : 0u;
+        F.T = (int32_t)std::min<int64_t>(1024, std::max<int64_t>(16, (tb / SB) / 16 * 16));
         const uint32_t T = (uint32_t)F.T, QW = (uint32_t)((B + 3) / 4);
-        const size_t lds = (size_t)T * B + 16 + 12 * QW + 4 * ((T + 1) & ~1u);
+        const size_t lds = (size_t)T * SB + 16 + 12 * QW + 4 * ((T + 1) & ~1u);
         DecColsK K;
         memset(&K, 0, sizeof(K));
         K.n = (int32_t)s->dfix.size();

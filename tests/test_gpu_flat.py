@@ -43,8 +43,10 @@ def flat_chain(rng):
         leaves.insert(rng.randint(0, len(leaves)), SVariableBytes())
     # >= 15 static bytes before the first var value (flat_plan's condition):
     # header words of the leading fixed leaves + their widths, else an SInt64 lead
-    nlead = next(j for j, x in enumerate(leaves) if x.width <= 0 and x.kind in ("string", "bytes"))
-    if 2 * (len(leaves) + 1) + sum(x.width for x in leaves[:nlead]) < 15:
+    while True:
+        nlead = next(j for j, x in enumerate(leaves) if x.width <= 0 and x.kind in ("string", "bytes"))
+        if 2 * (len(leaves) + 1) + sum(x.width for x in leaves[:nlead]) >= 15:
+            break
         leaves.insert(0, SInt64)
     return SChain(*leaves)
 
@@ -94,7 +96,8 @@ def check(chain, hc, mode, what, shift=False, off64=False, kernel=None):
                                  None, 0, 0, None) == 0, L.packos_last_error()
     T.cuda.synchronize()
     if kernel:   # the encoder under test actually ran (not a silent fallback)
-        assert L.packos_last_encoder().decode() == kernel, (what, L.packos_last_encoder())
+        ok = (kernel,) if isinstance(kernel, str) else kernel
+        assert L.packos_last_encoder().decode() in ok, (what, L.packos_last_encoder())
     o1 = offs.cpu().numpy().astype(np.uint64)
     assert np.array_equal(o1, o0), f"{what}: offsets differ"
     a1 = out[: int(o0[n])].cpu().numpy()
@@ -124,7 +127,10 @@ def test_flat_random_flat(seed, flat_on):
     chain = flat_chain(rng)
     n = [1, 127, 128, 129, 300, 1000, 2049][seed % 7]
     hc = HostColumns.from_rows(chain, rows(chain, n, seed * 11 + 5))
-    check(chain, hc, seed % 2, f"seed {seed}", shift=seed % 3 == 1, off64=seed % 4 == 3, kernel=flat_on)
+    # a wide static image leaves the streaming pass too little LDS for even a
+    # 1-KiB window: the chunk-gather pass then takes the chain
+    want = flat_on if flat_on == "flat" else ("flat_s", "flat")
+    check(chain, hc, seed % 2, f"seed {seed}", shift=seed % 3 == 1, off64=seed % 4 == 3, kernel=want)
 
 
 def test_flat_wide_fixed_leaf_falls_back():
