@@ -1055,7 +1055,11 @@ def test_checked_schema_decode_fast(seed):
     """Fixed layouts with value checks keep the tiled decoder; rows failing a
     check are re-decoded exactly (status from decode_blob)."""
     chain = rand_checked_chain(seed, allow_var=False, allow_null=False)
-    assert CompiledSchema(chain).decode_fast
+    # a named tuple whose names and schemas differ in length fails every
+    # decode (schema.go:1756-1758): such a schema never takes the fast path
+    names_bad = any(n.kind == "tuple" and n.names is not None and len(n.names) != len(n.children)
+                    for n, *_ in chain.walk())
+    assert CompiledSchema(chain).decode_fast == (not names_bad)
     hc = HostColumns.from_rows(chain, rand_checked_rows(chain, 3001, seed + 13, nil_p=0.0))
     arena, offs, _ = ob.encode(chain, hc, 0)
     B = CompiledSchema(chain).fixed_blob_size
