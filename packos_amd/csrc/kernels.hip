@@ -2231,9 +2231,23 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
 #define PACKOS_FLAT(K, NV) \
     hipLaunchKernelGGL((K<NV>), g, dim3(kFNT), F.lds_total, st, F, out_offsets, out, cap, (uint64_t)n, status)
             if (F.wbytes) {
-                if (F.nvar <= 1) PACKOS_FLAT(k_encode_flat_s, 1);
-                else if (F.nvar <= 2) PACKOS_FLAT(k_encode_flat_s, 2);
-                else PACKOS_FLAT(k_encode_flat_s, 4);
+                // lanes per blob by the mean blob (the arena per blob): 8 up to
+                // 112 B (<= 7 chunks + the shared edge), 16 up to 240 B, else a wave
+                const uint64_t mb = n ? cap / n : 0;
+                const int gl = s->tune.flat_gl ? s->tune.flat_gl : mb <= 112 ? 8 : mb <= 240 ? 16 : 64;
+#define PACKOS_FLATS(NV)                                                                  \
+    do {                                                                                  \
+        if (gl == 8) hipLaunchKernelGGL((k_encode_flat_s<NV, 8>), g, dim3(kFNT), F.lds_total, st, F, \
+                                        out_offsets, out, cap, (uint64_t)n, status);      \
+        else if (gl == 16) hipLaunchKernelGGL((k_encode_flat_s<NV, 16>), g, dim3(kFNT), F.lds_total, st, F, \
+                                              out_offsets, out, cap, (uint64_t)n, status); \
+        else hipLaunchKernelGGL((k_encode_flat_s<NV, 64>), g, dim3(kFNT), F.lds_total, st, F, \
+                                out_offsets, out, cap, (uint64_t)n, status);              \
+    } while (0)
+                if (F.nvar <= 1) PACKOS_FLATS(1);
+                else if (F.nvar <= 2) PACKOS_FLATS(2);
+                else PACKOS_FLATS(4);
+#undef PACKOS_FLATS
             } else {
                 if (F.nvar <= 1) PACKOS_FLAT(k_encode_flat, 1);
                 else if (F.nvar <= 2) PACKOS_FLAT(k_encode_flat, 2);
@@ -2361,7 +2375,9 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
         // staged rows padded by 16 B when the row stride would put every row's
         // dword k on few LDS banks (dword reads bank on (a/4) % 32)
         int pad = s->tune.dec_pad;
-        if (pad < 0) pad = (B % 16 == 0 && std::gcd<int64_t>(B / 4, 32) >= 8) ? 16 : 0;
+        // (A/B on the box, round 4: M 0.0997 -> 0.112 ms, C2 0.0307 -> 0.0327,
+        // C4 0.425 -> 0.462 with the pad: off unless asked for)
+        if (pad < 0) pad = 0;
         if (B % 16) pad = 0;
         F.pad = pad;
         const int64_t SB = B + pad;

@@ -108,17 +108,19 @@ def check(chain, hc, mode, what, shift=False, off64=False, kernel=None):
     assert np.array_equal(st.cpu().numpy().astype(np.uint32), s0), f"{what}: status differs"
 
 
-# PACKOS_FLAT_W: the streaming kernel's window bytes (default 12288; 64 cuts
-# nearly every blob across windows), 0 = the chunk-gather kernel
-FLAT_W = ["12288", "0", "64"]
-FLAT_NAME = {"0": "flat"}
+# (PACKOS_FLAT_W, PACKOS_FLAT_GL): the streaming kernel's window bytes
+# (default 12288; 64 cuts nearly every blob across windows; 0 = the
+# chunk-gather kernel) and lanes per blob (0 = by mean blob size, 8 / 16 lane
+# groups, 64 a wave per blob)
+FLAT_VARIANTS = [("12288", "0"), ("0", "0"), ("64", "64"), ("12288", "8"), ("12288", "16"), ("64", "8")]
 
 
-@pytest.fixture(autouse=True, params=FLAT_W, ids=lambda w: f"W{w}")
+@pytest.fixture(autouse=True, params=FLAT_VARIANTS, ids=lambda p: f"W{p[0]}-GL{p[1]}")
 def flat_on(request, monkeypatch):
     monkeypatch.setenv("PACKOS_ENC_FLAT", "1")   # read when the schema compiles
-    monkeypatch.setenv("PACKOS_FLAT_W", request.param)
-    return FLAT_NAME.get(request.param, "flat_s")
+    monkeypatch.setenv("PACKOS_FLAT_W", request.param[0])
+    monkeypatch.setenv("PACKOS_FLAT_GL", request.param[1])
+    return "flat" if request.param[0] == "0" else "flat_s"
 
 
 @pytest.mark.parametrize("seed", range(40))
