@@ -112,7 +112,7 @@ def check(chain, hc, mode, what, shift=False, off64=False, kernel=None):
 # (default 12288; 64 cuts nearly every blob across windows; 0 = the
 # chunk-gather kernel) and lanes per blob (0 = by mean blob size, 8 / 16 lane
 # groups, 64 a wave per blob)
-FLAT_VARIANTS = [("12288", "0"), ("0", "0"), ("64", "64"), ("12288", "8"), ("12288", "16"), ("64", "8")]
+FLAT_VARIANTS = [("8192", "0"), ("0", "0"), ("64", "64"), ("8192", "8"), ("4096", "16"), ("64", "8")]
 
 
 @pytest.fixture(autouse=True, params=FLAT_VARIANTS, ids=lambda p: f"W{p[0]}-GL{p[1]}")

@@ -11,13 +11,12 @@ b() {  # name, config, env...
   env "$@" timeout -k 10 200 python bench.py --config $cfg --steps 10 --warmup 2 --no-warm --no-cpu --no-host > gpurun_out/b_$nm.json 2> gpurun_out/b_$nm.err || exit 5
   line gpurun_out/b_$nm.json "$nm"
 }
-b C5_w12288 C5 PACKOS_FLAT_W=12288
-b C5_w0 C5 PACKOS_FLAT_W=0
 b C5_w8192 C5 PACKOS_FLAT_W=8192
+b C5_w0 C5 PACKOS_FLAT_W=0
 b C5_w4096 C5 PACKOS_FLAT_W=4096
-b C5_w12288_gl16 C5 PACKOS_FLAT_W=12288 PACKOS_FLAT_GL=16
+b C5_w12288 C5 PACKOS_FLAT_W=12288
+b C5_w8192_gl16 C5 PACKOS_FLAT_W=8192 PACKOS_FLAT_GL=16
 b C3_tiles C3 PACKOS_ENC_FLAT=0
-b C3_flat_w0 C3 PACKOS_ENC_FLAT=1 PACKOS_FLAT_W=0
-b C3_gl8 C3 PACKOS_ENC_FLAT=1 PACKOS_FLAT_GL=8
-b C3_gl16 C3 PACKOS_ENC_FLAT=1 PACKOS_FLAT_GL=16
-b C3_gl64 C3 PACKOS_ENC_FLAT=1 PACKOS_FLAT_GL=64
+b C3_gl8_w4096 C3 PACKOS_ENC_FLAT=1 PACKOS_FLAT_GL=8 PACKOS_FLAT_W=4096
+b C3_gl8_w8192 C3 PACKOS_ENC_FLAT=1 PACKOS_FLAT_GL=8 PACKOS_FLAT_W=8192
+b C3_gl16_w4096 C3 PACKOS_ENC_FLAT=1 PACKOS_FLAT_GL=16 PACKOS_FLAT_W=4096
