@@ -51,7 +51,7 @@ struct Tune {
     int dec_pad = -1;            // PACKOS_DEC_PAD: staged row padding of the fixed decoder (-1 auto, 0, 16)
     int enc_flat = 2;            // PACKOS_ENC_FLAT: 0 never, 1 always, 2 auto (large blobs)
     int flat_gl = 0;             // PACKOS_FLAT_GL: lanes per blob of the streaming pass (8 / 16 / 64; 0 = by blob size)
-    int flat_w = 8192;           // PACKOS_FLAT_W: streaming flat encoder: var bytes per window (0: the chunk-gather kernel)
+    int flat_w = 0;              // PACKOS_FLAT_W: streaming flat encoder, var bytes per window (0: the chunk-gather kernel)
 };
 
 struct DeviceTables {
