@@ -1331,7 +1331,19 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
         struct { uint8_t* dst; uint32_t blob_off, flags, magic; } L = {K.dst[c], K.blob_off[c], K.flags[c], K.magic[c]};
         const uint32_t w = K.width[c], R = rows * w, D = R >> 2;
         uint32_t* dst = (uint32_t*)(L.dst + blob0 * w);   // 4-B aligned: T*w % 4 == 0, base 16-B aligned
-        if ((w & 3) == 0) {
+        if ((w & 15) == 0 && (SB & 15) == 0 && !(L.flags & 3u)) {   // flags bit 1: PACKOS_DEC_W16=0
+            // 16-B units (a string / bytes column of 16k bytes): a unit lies inside
+            // one row, at the same offset mod 16 in every row (SB % 16 == 0), so
+            // two ds_read_b128 + a shift chosen by a scalar branch per unit and one
+            // 1-KiB-per-wave NT store: a quarter of the dword path's iterations
+            typedef __attribute__((address_space(1))) u32x4 g_v4;
+            g_v4* dst16 = (g_v4*)(L.dst + blob0 * w);
+            const uint32_t U = R >> 4, m = L.blob_off & 15u;
+            for (uint32_t u = tid; u < U; u += kBlock) {
+                const uint32_t b = 16 * u, j = __umulhi(b, L.magic);
+                __builtin_nontemporal_store(lds16u(lds_raw, j * SB + L.blob_off + (b - j * w), m), dst16 + u);
+            }
+        } else if ((w & 3) == 0) {
             for (uint32_t d = tid; d < D; d += kBlock) {
                 const uint32_t b = 4 * d;
                 const uint32_t j = __umulhi(b, L.magic);
@@ -2393,7 +2405,7 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
             K.dst[c] = dc.data[f.col];
             K.width[c] = f.width;
             K.blob_off[c] = f.blob_off;
-            K.flags[c] = f.flags;
+            K.flags[c] = f.flags | (s->tune.dec_w16 ? 0u : 2u);
             K.magic[c] = f.magic;
         }
         if (s->ext)
