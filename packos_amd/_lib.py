@@ -118,7 +118,8 @@ def lib():
     L.packos_strerror.argtypes = [i32]
     L.packos_strerror.restype = C.c_char_p
     L.packos_last_error.restype = C.c_char_p
-    L.packos_last_encoder.restype = C.c_char_p
+    if os.environ.get("PACKOS_LIB") is None or hasattr(L, "packos_last_encoder"):   # older builds in A/Bs lack it
+        L.packos_last_encoder.restype = C.c_char_p
     L.packos_abi_version.restype = i32
     got = L.packos_abi_version()
     if got != ABI_VERSION:   # a stale or foreign .so would read packos_column with the wrong stride

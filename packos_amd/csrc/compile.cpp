@@ -855,7 +855,6 @@ void read_tune(Tune& t) {
     if (const char* e = getenv("PACKOS_DEC_TILE_BYTES")) t.dec_tile_bytes = std::min(49152, std::max(1024, atoi(e)));
     if (const char* e = getenv("PACKOS_ENC_FLAT")) t.enc_flat = atoi(e);
     if (const char* e = getenv("PACKOS_DEC_W16")) t.dec_w16 = atoi(e) != 0;
-    if (const char* e = getenv("PACKOS_DEC_PAD")) t.dec_pad = atoi(e) == 16 ? 16 : atoi(e) == 0 ? 0 : -1;
     if (const char* e = getenv("PACKOS_FLAT_GL")) t.flat_gl = atoi(e) == 8 || atoi(e) == 16 || atoi(e) == 64 ? atoi(e) : 0;
     if (const char* e = getenv("PACKOS_FLAT_W")) t.flat_w = std::max(0, std::min(24576, atoi(e) & ~15));
 }

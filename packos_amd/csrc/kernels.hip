@@ -1230,10 +1230,9 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
     uint32_t* lds = (uint32_t*)lds_raw;
     const uint32_t B = (uint32_t)F.B, T = (uint32_t)F.T, QW = (B + 3) >> 2;
-    // staged row stride: B, or B + 16 (F.pad) so that rows whose stride is a
-    // multiple of 128 B do not all start on one LDS bank (column reads gather
-    // one dword per row: 16-way conflicts for M's 256-B rows)
-    const uint32_t SB = B + (uint32_t)F.pad;
+    // staged row stride (rows padded to B + 16 measured slower: M decode 0.0997
+    // -> 0.112 ms with 2.6x fewer bank-conflict cycles; round-4 A/B)
+    const uint32_t SB = B;
     const uint64_t blob0 = (uint64_t)blockIdx.x * T;
     const uint32_t rows = (uint32_t)min((uint64_t)T, n - blob0);
     const int tid = threadIdx.x;
@@ -1262,22 +1261,9 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
         const uint8_t* src = arena + base;
         const uint32_t n16 = bytes >> 4, lane = tid & 63, c00 = tid & ~63u;
         const uint32_t lds0 = (uint32_t)(uintptr_t)lds_raw;
-        if (F.pad == 0) {
-            for (uint32_t c0 = c00; c0 < n16; c0 += kBlock)
-                if (c0 + lane < n16) dma16(src + 16u * (c0 + lane), __builtin_amdgcn_readfirstlane(lds0 + 16u * c0));
-            for (uint32_t k = n16 * 16 + tid; k < bytes; k += kBlock) lds_raw[k] = src[k];
-        } else {
-            // padded rows: LDS chunk L (written by lane L % 64 of a full-width
-            // DMA instruction) holds chunk c = L % cpr of row j = L / cpr, the
-            // global chunk j * cpb + c; the pad chunk (c == cpb) is not loaded
-            const uint32_t cpr = SB >> 4, cpb = B >> 4, NL = (n16 / cpb + 1) * cpr;
-            for (uint32_t c0 = c00; c0 < NL; c0 += kBlock) {
-                const uint32_t L = c0 + lane, j = __umulhi(L, (uint32_t)F.b_magic), c = L - j * cpr;
-                const uint32_t g = j * cpb + c;
-                if (c < cpb && g < n16) dma16(src + 16u * g, __builtin_amdgcn_readfirstlane(lds0 + 16u * c0));
-            }
-            for (uint32_t k = n16 * 16 + tid; k < bytes; k += kBlock) lds_raw[(k / B) * SB + k % B] = src[k];
-        }
+        for (uint32_t c0 = c00; c0 < n16; c0 += kBlock)
+            if (c0 + lane < n16) dma16(src + 16u * (c0 + lane), __builtin_amdgcn_readfirstlane(lds0 + 16u * c0));
+        for (uint32_t k = n16 * 16 + tid; k < bytes; k += kBlock) lds_raw[k] = src[k];
     }
     if (offs) {
         for (uint32_t j = tid; j <= rows; j += kBlock) ok &= offs[blob0 + j] == base + (uint64_t)j * B;
@@ -2384,19 +2370,9 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
         // small blobs the larger tile loses more to fewer workgroups (C2 +7 %)
         int64_t tb = B >= 128 ? kDecTileBytesLarge : kDecTileBytes;
         if (s->tune.dec_tile_bytes) tb = s->tune.dec_tile_bytes;
-        // staged rows padded by 16 B when the row stride would put every row's
-        // dword k on few LDS banks (dword reads bank on (a/4) % 32)
-        int pad = s->tune.dec_pad;
-        // (A/B on the box, round 4: M 0.0997 -> 0.112 ms, C2 0.0307 -> 0.0327,
-        // C4 0.425 -> 0.462 with the pad: off unless asked for)
-        if (pad < 0) pad = 0;
-        if (B % 16) pad = 0;
-        F.pad = pad;
-        const int64_t SB = B + pad;
-        F.b_magic = pad ? (uint32_t)(((1ull << 32) + SB / 16 - 1) / (SB / 16)) : 0u;
-        F.T = (int32_t)std::min<int64_t>(1024, std::max<int64_t>(16, (tb / SB) / 16 * 16));
+        F.T = (int32_t)std::min<int64_t>(1024, std::max<int64_t>(16, (tb / B) / 16 * 16));
         const uint32_t T = (uint32_t)F.T, QW = (uint32_t)((B + 3) / 4);
-        const size_t lds = (size_t)T * SB + 16 + 12 * QW + 4 * ((T + 1) & ~1u);
+        const size_t lds = (size_t)T * B + 16 + 12 * QW + 4 * ((T + 1) & ~1u);
         DecColsK K;
         memset(&K, 0, sizeof(K));
         K.n = (int32_t)s->dfix.size();

@@ -49,7 +49,6 @@ struct Tune {
     bool decode_generic = false;
     int dec_tile_bytes = 0;      // 0: 24 KB for B >= 128, else 16 KB
     bool dec_w16 = true;         // PACKOS_DEC_W16=0: the fixed decoder's dword path for 16k-byte columns too
-    int dec_pad = -1;            // PACKOS_DEC_PAD: staged row padding of the fixed decoder (-1 auto, 0, 16)
     int enc_flat = 2;            // PACKOS_ENC_FLAT: 0 never, 1 always, 2 auto (large blobs)
     int flat_gl = 0;             // PACKOS_FLAT_GL: lanes per blob of the streaming pass (8 / 16 / 64; 0 = by blob size)
     int flat_w = 0;              // PACKOS_FLAT_W: streaming flat encoder, var bytes per window (0: the chunk-gather kernel)
