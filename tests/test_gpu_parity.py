@@ -523,6 +523,31 @@ def test_random_decode_roundtrip(seed):
         assert (st == 0).all()
 
 
+@pytest.mark.parametrize("nested", [False, True])
+def test_named_tuple_rules(nested):
+    """TupleSchemaNamed (schema.go:1726-1810), explicit statuses as well as
+    the oracle's: FieldNames shorter than Schemas -> encoding a present value
+    fails (ErrEncode wrapping ErrConstraintViolated, or ErrInvalidFormat when a
+    parent tuple wraps it), a nil one encodes; every decode fails at position
+    0 (top level) or as ErrInvalidFormat at the parent's position (nested)."""
+    from packos_amd.schema import STupleNamed
+    bad = STupleNamed(["a"], SInt32, SInt16)
+    chain = SChain(SInt16, STuple(bad) if nested else bad, SInt16)
+    rows = [[1, [[7, 8]] if nested else [7, 8], 2], [3, [None] if nested else None, 4]] * 50
+    hc = HostColumns.from_rows(chain, rows)
+    assert_same_encoding(chain, hc, 0, "named mismatch")
+    _, _, st = gpu_encode(chain, hc, 0)
+    enc_present = 4 | ((1 if nested else 3) << 24)
+    assert st[0] == enc_present and st[1] == 0
+    good = STupleNamed(["a", "b"], SInt32, SInt16)
+    ok_chain = SChain(SInt16, STuple(good) if nested else good, SInt16)
+    arena, offs, _ = ob.encode(ok_chain, HostColumns.from_rows(ok_chain, rows), 0)
+    st = assert_same_decode(chain, arena, offs, len(rows), "named mismatch decode")
+    # the names check runs before precheck: a nil named tuple fails too
+    want = (1 | (2 << 8)) if nested else (3 | (1 << 8))
+    assert int(st[0]) == want and int(st[1]) == want
+
+
 @pytest.mark.parametrize("k,w", [(6, 8), (12, 8), (15, 8), (15, 4), (13, 8)])
 def test_decode_long_static_prefix(k, w):
     """A flat chain whose static prefix (header block + k fixed fields) is
