@@ -201,9 +201,14 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCol
 // m0 + 16*l (wave-uniform m0).  Written as asm so the compiler neither waits
 // for it (it would drain with vmcnt(0) before every LDS read or barrier) nor
 // reorders LDS accesses across it: every wait for it is explicit.
+#ifdef PACKOS_DMA_NT
+#define PACKOS_DMA_POLICY " nt"
+#else
+#define PACKOS_DMA_POLICY ""
+#endif
 __device__ __forceinline__ void dma16(const uint8_t* gsrc, uint32_t lds_addr) {
     uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" PACKOS_DMA_POLICY "\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(gsrc), "s"(lds_addr)
                  : "memory");
