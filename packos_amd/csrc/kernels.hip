@@ -201,14 +201,19 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_dw(FixProgram P, EncCol
 // m0 + 16*l (wave-uniform m0).  Written as asm so the compiler neither waits
 // for it (it would drain with vmcnt(0) before every LDS read or barrier) nor
 // reorders LDS accesses across it: every wait for it is explicit.
-#ifdef PACKOS_DMA_NT
-#define PACKOS_DMA_POLICY " nt"
-#else
-#define PACKOS_DMA_POLICY ""
-#endif
 __device__ __forceinline__ void dma16(const uint8_t* gsrc, uint32_t lds_addr) {
     uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" PACKOS_DMA_POLICY "\n\ts_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_addr)
+                 : "memory");
+}
+// the same, non-temporal: rows read once by the fixed-layout kernels (round-4
+// A/B on the box: M encode 0.0889 -> 0.0878 ms, M decode 0.1015 -> 0.0982 ms,
+// C4 encode 0.332 -> 0.328 ms; the var tile encoder loses with it, 0.050 -> 0.053)
+__device__ __forceinline__ void dma16nt(const uint8_t* gsrc, uint32_t lds_addr) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(gsrc), "s"(lds_addr)
                  : "memory");
@@ -248,7 +253,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_tile(FixProgram P, FixS
         // the kernel argument (a scalar load + wait) before every DMA
         const uint32_t lbase = lds0 + S.c[g].lds_off;
         for (uint32_t c0 = wv * kWave; c0 < nch; c0 += kBlock) {
-            if (c0 + lane < nch) dma16(cbase + (c0 + lane) * 16u, __builtin_amdgcn_readfirstlane(lbase + c0 * 16u));
+            if (c0 + lane < nch) dma16nt(cbase + (c0 + lane) * 16u, __builtin_amdgcn_readfirstlane(lbase + c0 * 16u));
         }
     }
     // descriptors (their global loads queue behind the DMA)
@@ -1267,7 +1272,7 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
         const uint32_t n16 = bytes >> 4, lane = tid & 63, c00 = tid & ~63u;
         const uint32_t lds0 = (uint32_t)(uintptr_t)lds_raw;
         for (uint32_t c0 = c00; c0 < n16; c0 += kBlock)
-            if (c0 + lane < n16) dma16(src + 16u * (c0 + lane), __builtin_amdgcn_readfirstlane(lds0 + 16u * c0));
+            if (c0 + lane < n16) dma16nt(src + 16u * (c0 + lane), __builtin_amdgcn_readfirstlane(lds0 + 16u * c0));
         for (uint32_t k = n16 * 16 + tid; k < bytes; k += kBlock) lds_raw[k] = src[k];
     }
     if (offs) {
