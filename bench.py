@@ -225,7 +225,7 @@ def decode_parity(cfg, arena, offsets, stride, n, gout, gst, threads):
     columns (fixed values, validity, views) for every blob that decodes."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bridge as ob  # checker only
-    o_out, o_st = ob.decode(cfg.chain, arena, offsets, n, stride=stride, nthreads=threads)
+    o_out, o_st = ob.decode(cfg.chain, arena, offsets, n, stride=stride, nthreads=threads, mode=cfg.mode)
     g_st = gst[:n].cpu().numpy().astype(np.uint32)
     same = bool(np.array_equal(o_st[:n], g_st))
     ok = o_st[:n] == 0
