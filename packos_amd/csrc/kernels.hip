@@ -260,8 +260,20 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_tile(FixProgram P, FixS
     const DwDesc* dd = P.tdw + q;
     const uint32_t cval = dd->cval;
     const DwSeg sg = dd->seg[0];
-    uint32_t a = (uint32_t)sg.a + s * sg.w;  // LDS byte address of this thread's first dword
-    const uint32_t xs = R * sg.w, xm = sg.mask;
+    // a wave stores G = 64 / Q4 consecutive blobs per instruction (256 B) and
+    // its PER instructions continue that run: wave w covers blobs
+    // [w PER G, (w + 1) PER G) of the tile (M encode 0.0875 -> 0.0867 ms, A/B;
+    // PACKOS_FIXT_STRIDED: the round-3 order, blob groups R apart)
+    // (when Q4 divides 64: a wave holds whole blobs; else the strided order)
+#ifndef PACKOS_FIXT_STRIDED
+    const bool contig = Q4 <= (uint32_t)kWave && (uint32_t)kWave % Q4 == 0;
+#else
+    const bool contig = false;
+#endif
+    const uint32_t G = contig ? (uint32_t)kWave / Q4 : 1u;
+    const uint32_t b0s = contig ? (s / G) * PER * G + s % G : s;   // this thread's first blob
+    uint32_t a = (uint32_t)sg.a + b0s * sg.w;   // LDS byte address of this thread's first dword
+    const uint32_t xs = (contig ? G : R) * sg.w, xm = sg.mask;
     const uint32_t nxi = T * (uint32_t)P.nx;
     DwDesc xd;  // this thread's first X item
     if (tid < nxi) xd = P.xdw[tid % (uint32_t)P.nx];
@@ -287,8 +299,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_tile(FixProgram P, FixS
         __syncthreads();
     }
     if (s < R) {  // R * Q4 <= 256: the rest of the threads idle here
-        uint32_t* o32 = (uint32_t*)(out + blob0 * B) + s * Q4 + q;
-        const uint32_t ostep = R * Q4;
+        uint32_t* o32 = (uint32_t*)(out + blob0 * B) + b0s * Q4 + q;
+        const uint32_t ostep = (contig ? G : R) * Q4;
 #pragma unroll
         for (int it = 0; it < PER; it++) {
             uint32_t val = cval;
