@@ -1333,19 +1333,8 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
         }
         if (bad) fail[j] = 1;
     }
-    // 3. columns: uniform walk over the columns; each wave writes a contiguous
-    //    quarter of the column's output units, consecutive lanes consecutive
-    //    units (256-B or 1-KiB stores, one run per wave; PACKOS_DEC_STRIDED:
-    //    the four waves interleaved unit by unit)
-    const uint32_t wv = (uint32_t)tid / kWave, ln = (uint32_t)tid % kWave;
-    auto wrange = [&](uint32_t N, uint32_t& b, uint32_t& e, uint32_t& st) {
-#ifdef PACKOS_DEC_STRIDED
-        b = (uint32_t)tid; e = N; st = kBlock;
-#else
-        const uint32_t ch = (((N + 3u) >> 2) + 63u) & ~63u;
-        b = wv * ch + ln; e = min(N, wv * ch + ch); st = kWave;
-#endif
-    };
+    // 3. columns: uniform walk over the columns; threads stride the column's
+    //    output dwords (consecutive lanes -> consecutive dwords: 256-B stores)
     for (int c = 0; c < K.n; c++) {
         struct { uint8_t* dst; uint32_t blob_off, flags, magic; } L = {K.dst[c], K.blob_off[c], K.flags[c], K.magic[c]};
         const uint32_t w = K.width[c], R = rows * w, D = R >> 2;
@@ -1358,33 +1347,25 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
             typedef __attribute__((address_space(1))) u32x4 g_v4;
             g_v4* dst16 = (g_v4*)(L.dst + blob0 * w);
             const uint32_t U = R >> 4, m = L.blob_off & 15u;
-            uint32_t ub, ue, us;
-            wrange(U, ub, ue, us);
-            for (uint32_t u = ub; u < ue; u += us) {
+            for (uint32_t u = tid; u < U; u += kBlock) {
                 const uint32_t b = 16 * u, j = __umulhi(b, L.magic);
                 __builtin_nontemporal_store(lds16u(lds_raw, j * SB + L.blob_off + (b - j * w), m), dst16 + u);
             }
         } else if ((w & 3) == 0) {
-            uint32_t db, de, ds;
-            wrange(D, db, de, ds);
-            for (uint32_t d = db; d < de; d += ds) {
+            for (uint32_t d = tid; d < D; d += kBlock) {
                 const uint32_t b = 4 * d;
                 const uint32_t j = __umulhi(b, L.magic);
                 const uint32_t a = j * SB + L.blob_off + (b - j * w);
                 __builtin_nontemporal_store(lds_bytes4(lds, a), dst + d);
             }
         } else if (w == 2) {   // a dword = rows 2d, 2d+1
-            uint32_t db, de, ds;
-            wrange(D, db, de, ds);
-            for (uint32_t d = db; d < de; d += ds) {
+            for (uint32_t d = tid; d < D; d += kBlock) {
                 const uint32_t a = 2 * d * SB + L.blob_off;
                 const uint32_t x = (lds_bytes4(lds, a) & 0xFFFFu) | (lds_bytes4(lds, a + SB) << 16);
                 __builtin_nontemporal_store(x, dst + d);
             }
         } else if (w > 4 && !(L.flags & 1u)) {   // most dwords sit inside one row
-            uint32_t db, de, ds;
-            wrange(D, db, de, ds);
-            for (uint32_t d = db; d < de; d += ds) {
+            for (uint32_t d = tid; d < D; d += kBlock) {
                 const uint32_t b = 4 * d;
                 const uint32_t j = __umulhi(b, L.magic);
                 const uint32_t r = b - j * w;
@@ -1399,9 +1380,7 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
                 __builtin_nontemporal_store(x, dst + d);
             }
         } else {
-            uint32_t db, de, ds;
-            wrange(D, db, de, ds);
-            for (uint32_t d = db; d < de; d += ds) {
+            for (uint32_t d = tid; d < D; d += kBlock) {
                 uint32_t x = 0;
 #pragma unroll
                 for (int y = 0; y < 4; y++) {
