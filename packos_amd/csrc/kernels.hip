@@ -1137,34 +1137,57 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECWIN_ATTR void k_decode_win(DecPro
     DecNode* lnodes = (DecNode*)ptab;
     int32_t* lkids = (int32_t*)(ptab + ((P.n_nodes * sizeof(DecNode) + 15) & ~15));
     uint8_t* llits = (uint8_t*)lkids + ((P.n_kids * 4 + 15) & ~15);
-    for (int x = tid; x < P.n_nodes; x += kBlock) lnodes[x] = P.nodes[x];
-    for (int x = tid; x < P.n_kids; x += kBlock) lkids[x] = P.kids[x];
-    for (int x = tid; x < P.n_lits; x += kBlock) llits[x] = P.lits[x];
     const uint64_t lo = (uint64_t)blockIdx.x * kBlock, i = lo + tid;
     const uint32_t rows = (uint32_t)min((uint64_t)kBlock, n - lo);
-    uint64_t a0 = 0, a1 = 0;
-    if (i < n) {
-        a0 = offs ? offs[i] : i * stride;
-        a1 = offs ? offs[i + 1] : (i + 1) * stride;
+    // the tile's byte range (two scalar loads, one round trip)
+    typedef __attribute__((address_space(4))) const uint64_t c_u64;
+    uint64_t t0 = lo * stride, t1 = (lo + rows) * stride;
+    if (offs) {
+        t0 = ((c_u64*)(uintptr_t)offs)[lo];
+        t1 = ((c_u64*)(uintptr_t)offs)[lo + rows];
+    }
+    // the program tables and this blob's offsets: one round of loads (a
+    // load -> LDS loop per table would wait once per table before the DMA)
+    const uint32_t nnw = (uint32_t)P.n_nodes * (uint32_t)(sizeof(DecNode) / 4);
+    const uint32_t* gnodes = (const uint32_t*)P.nodes;
+    uint32_t pn0 = 0, pn1 = 0, pk = 0;
+    uint8_t pl = 0;
+    if ((uint32_t)tid < nnw) pn0 = gnodes[tid];
+    if ((uint32_t)tid + kBlock < nnw) pn1 = gnodes[tid + kBlock];
+    if (tid < P.n_kids) pk = P.kids[tid];
+    if (tid < P.n_lits) pl = P.lits[tid];
+    uint64_t a0 = i * stride, a1 = (i + 1) * stride;
+    if (i >= n) a0 = a1 = 0;
+    else if (offs) {   // both in one block: a wait between them otherwise
+        a0 = offs[i];
+        a1 = offs[i + 1];
     }
     // Small blobs: when the tile's whole byte range fits the window memory,
     // stage it once with coalesced LDS-DMA and let every blob read from there
     // (same reader, one shared window).  Otherwise each blob's first
     // kDecWinChunks * 16 bytes go to its own window (headers + fixed fields sit
     // at the front; var values are returned as views and never read).
-    typedef __attribute__((address_space(4))) const uint64_t c_u64;
-    const uint64_t t0 = offs ? ((c_u64*)(uintptr_t)offs)[lo] : lo * stride;
-    const uint64_t t1 = offs ? ((c_u64*)(uintptr_t)offs)[lo + rows] : (lo + rows) * stride;
     const uint64_t tb = t0 & ~15ull;
     const bool tile_mode = t1 >= t0 && t1 - tb <= (uint64_t)sizeof(win) && ((uintptr_t)arena & 15) == 0;
     uint8_t* w;
     uint64_t b0;
     uint32_t wbytes;
+    auto store_program = [&]() {
+        uint32_t* lnw = (uint32_t*)lnodes;
+        if ((uint32_t)tid < nnw) lnw[tid] = pn0;
+        if ((uint32_t)tid + kBlock < nnw) lnw[tid + kBlock] = pn1;
+        for (uint32_t x = tid + 2 * kBlock; x < nnw; x += kBlock) lnw[x] = gnodes[x];
+        if (tid < P.n_kids) lkids[tid] = pk;
+        for (int x = tid + kBlock; x < P.n_kids; x += kBlock) lkids[x] = P.kids[x];
+        if (tid < P.n_lits) llits[tid] = pl;
+        for (int x = tid + kBlock; x < P.n_lits; x += kBlock) llits[x] = P.lits[x];
+    };
     if (tile_mode) {
         const uint32_t nch = (uint32_t)((t1 - tb + 15) >> 4), lane = tid & 63, c00 = tid & ~63u;
         const uint32_t lds0 = (uint32_t)(uintptr_t)win;
         for (uint32_t c0 = c00; c0 < nch; c0 += kBlock)
             if (c0 + lane < nch) dma16(arena + tb + 16u * (c0 + lane), __builtin_amdgcn_readfirstlane(lds0 + 16u * c0));
+        store_program();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         w = win;
         b0 = tb;
@@ -1181,6 +1204,7 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECWIN_ATTR void k_decode_win(DecPro
 #pragma unroll
         for (int c = 0; c < WC; c++)
             if ((uint32_t)c < nch) v[c] = *(const g_u32x4*)(arena + b0 + 16 * c);
+        store_program();
         uint32_t* w32 = (uint32_t*)w;
 #pragma unroll
         for (int c = 0; c < WC; c++)
@@ -1264,21 +1288,23 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
     // the tile base is one scalar load; whether the tile's blobs really lie
     // back to back at stride B is checked while the staging DMA is in flight
     typedef __attribute__((address_space(4))) const uint64_t c_u64;
-    const uint64_t base = offs ? ((c_u64*)(uintptr_t)offs)[blob0] : blob0 * B;
+    // the tile's start and end offsets: two scalar loads in one round trip,
+    // the only memory latency in front of the staging DMA (the check table's
+    // copy to LDS queues behind the DMA)
+    uint64_t base = blob0 * B, end = base + (uint64_t)rows * B;
+    if (offs) {
+        base = ((c_u64*)(uintptr_t)offs)[blob0];
+        end = ((c_u64*)(uintptr_t)offs)[blob0 + rows];
+    }
     const bool aligned_base = (base & 15) == 0;
     bool ok = true;
-    for (uint32_t q = tid; q < 3u * (uint32_t)F.n_chk; q += kBlock) chk[q] = F.chk[q];
-    for (uint32_t j = tid; j < rows; j += kBlock) fail[j] = 0;
     // 1. stage: global -> LDS with global_load_lds_dwordx4 (every chunk of the
     //    tile in flight at once; a load -> ds_write loop waits per chunk)
     //    Staged bytes stop at the tile's end offset: a truncated or corrupt
     //    batch must not read past what its offsets cover (the tile then fails
     //    the contiguity check and takes the per-blob path below).
     uint32_t bytes = rows * B;
-    if (offs) {
-        const uint64_t end = ((c_u64*)(uintptr_t)offs)[blob0 + rows];
-        bytes = end <= base ? 0u : (uint32_t)min((uint64_t)bytes, end - base);
-    }
+    if (offs) bytes = end <= base ? 0u : (uint32_t)min((uint64_t)bytes, end - base);
     if (aligned_base) {
         const uint8_t* src = arena + base;
         const uint32_t n16 = bytes >> 4, lane = tid & 63, c00 = tid & ~63u;
@@ -1287,8 +1313,21 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
             if (c0 + lane < n16) dma16nt(src + 16u * (c0 + lane), __builtin_amdgcn_readfirstlane(lds0 + 16u * c0));
         for (uint32_t k = n16 * 16 + tid; k < bytes; k += kBlock) lds_raw[k] = src[k];
     }
+    // the check table and the contiguity check's offsets: one round of loads,
+    // queued behind the DMA (a load -> use loop per table would wait twice)
+    const uint32_t nchk = 3u * (uint32_t)F.n_chk;
+    {
+        uint32_t cv = 0;
+        uint64_t ov = 0;
+        if ((uint32_t)tid < nchk) cv = F.chk[tid];
+        if (offs && (uint32_t)tid <= rows) ov = offs[blob0 + tid];
+        if ((uint32_t)tid < nchk) chk[tid] = cv;
+        if (offs && (uint32_t)tid <= rows) ok &= ov == base + (uint64_t)tid * B;
+    }
+    for (uint32_t q = tid + kBlock; q < nchk; q += kBlock) chk[q] = F.chk[q];
+    for (uint32_t j = tid; j < rows; j += kBlock) fail[j] = 0;
     if (offs) {
-        for (uint32_t j = tid; j <= rows; j += kBlock) ok &= offs[blob0 + j] == base + (uint64_t)j * B;
+        for (uint32_t j = tid + kBlock; j <= rows; j += kBlock) ok &= offs[blob0 + j] == base + (uint64_t)j * B;
         ok &= aligned_base;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1518,6 +1557,8 @@ __global__ __launch_bounds__(kBlock) void k_get_field(const uint8_t* __restrict_
                                                       uint8_t* __restrict__ status) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    // (one block with both loads merges them into a 16-B load per lane:
+    // M GetInt 0.0279 -> 0.0283 ms, A/B; kept as two loads)
     const uint64_t a0 = offs ? offs[i] : i * stride;
     const uint64_t a1 = offs ? offs[i + 1] : (i + 1) * stride;
     GWin r;
@@ -1676,6 +1717,8 @@ __global__ __launch_bounds__(kBlock) void k_get_map(const uint8_t* __restrict__ 
                                                     uint8_t* __restrict__ val_tag, uint8_t* __restrict__ status) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    // (one block with both loads merges them into a 16-B load per lane:
+    // M GetInt 0.0279 -> 0.0283 ms, A/B; kept as two loads)
     const uint64_t a0 = offs ? offs[i] : i * stride;
     const uint64_t a1 = offs ? offs[i + 1] : (i + 1) * stride;
     GWin r;
