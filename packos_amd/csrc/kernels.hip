@@ -30,6 +30,9 @@
 #include <numeric>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <utility>
 #include <vector>
 
 #include "schema_impl.h"
@@ -1268,18 +1271,156 @@ struct DecColsK {
 
 __device__ __forceinline__ uint32_t lds_u8(const uint32_t* lds, uint32_t a) { return (lds[a >> 2] >> (8 * (a & 3))) & 0xFFu; }
 
+// Steps 2-4 of a staged tile (constant-byte and value checks -> fail flags,
+// column stores, validity) by NCT threads, this one being thread ct; the
+// tile's rows start at lds_raw.  Then, after a barrier, dfix_status: every
+// row's status, failed rows through decode_blob (clear: reset the row's fail
+// flag for the next tile of a persistent workgroup).
+template <int NCT>
+__device__ __forceinline__ void dfix_tile(const DecFixProgram& F, const DecProgram& P, const DecCols& cols,
+                                          const DecColsK& K, const uint8_t* lds_raw, const uint32_t* chk,
+                                          uint32_t* fail, uint64_t blob0, uint32_t rows, uint32_t ct) {
+    const uint32_t* lds = (const uint32_t*)lds_raw;
+    const uint32_t B = (uint32_t)F.B, SB = B;
+    // 2. constant-byte check, over the blob dwords that HOLD constant bytes
+    //    (header words, literals: 5 of 64 for metric M; list built at compile)
+    {
+        const uint32_t nq = (uint32_t)F.n_chk;
+        const uint32_t nq_magic = nq > 1 ? (uint32_t)((0x100000000ull + nq - 1) / nq) : 0u;
+        for (uint32_t e = ct; e < rows * nq; e += NCT) {
+            const uint32_t j = nq > 1 ? __umulhi(e, nq_magic) : e;
+            const uint32_t* c = chk + 3 * (e - j * nq);
+            const uint32_t a = j * SB + 4 * c[0];   // blob dword q (B % 4 == 0: aligned)
+            const uint32_t v = (B & 3) == 0 ? lds[a >> 2] : lds_bytes4(lds, a);
+            if ((v & c[1]) != c[2]) fail[j] = 1;
+        }
+    }
+    // 2b. value checks of fixed leaves (Range, Prefix/Suffix of fixed strings):
+    //    a failing row takes the exact per-blob path, which reports it
+    for (uint32_t e = ct; e < rows * (uint32_t)F.n_vchk; e += NCT) {
+        const uint32_t j = e / (uint32_t)F.n_vchk;
+        const DecChk c = F.vchk[e - j * (uint32_t)F.n_vchk];
+        const uint32_t a = j * SB + c.blob_off;
+        bool bad;
+        if (c.flags & CHK_RANGE) {
+            uint64_t u = 0;
+            for (uint32_t b = 0; b < c.width; b++) u |= (uint64_t)lds_u8(lds, a + b) << (8 * b);
+            const int sh = 64 - 8 * (int)c.width;
+            const int64_t v = (int64_t)(u << sh) >> sh;
+            bad = ((c.flags & CHK_MIN) && v < c.rmin) || ((c.flags & CHK_MAX) && v > c.rmax);
+        } else {
+            bad = c.lit_len > c.width;
+            const uint32_t at = (c.flags & CHK_PREFIX) ? 0u : c.width - c.lit_len;
+            for (uint32_t b = 0; !bad && b < c.lit_len; b++) bad = lds_u8(lds, a + at + b) != P.lits[c.lit + b];
+        }
+        if (bad) fail[j] = 1;
+    }
+    // 3. columns: uniform walk over the columns; threads stride the column's
+    //    output dwords (consecutive lanes -> consecutive dwords: 256-B stores)
+    for (int c = 0; c < K.n; c++) {
+        struct { uint8_t* dst; uint32_t blob_off, flags, magic; } L = {K.dst[c], K.blob_off[c], K.flags[c], K.magic[c]};
+        const uint32_t w = K.width[c], R = rows * w, D = R >> 2;
+        uint32_t* dst = (uint32_t*)(L.dst + blob0 * w);   // 4-B aligned: T*w % 4 == 0, base 16-B aligned
+        if ((w & 15) == 0 && (SB & 15) == 0 && !(L.flags & 3u)) {   // flags bit 1: PACKOS_DEC_W16=0
+            // 16-B units (a string / bytes column of 16k bytes): a unit lies inside
+            // one row, at the same offset mod 16 in every row (SB % 16 == 0), so
+            // two ds_read_b128 + a shift chosen by a scalar branch per unit and one
+            // 1-KiB-per-wave NT store: a quarter of the dword path's iterations
+            typedef __attribute__((address_space(1))) u32x4 g_v4;
+            g_v4* dst16 = (g_v4*)(L.dst + blob0 * w);
+            const uint32_t U = R >> 4, m = L.blob_off & 15u;
+            for (uint32_t u = ct; u < U; u += NCT) {
+                const uint32_t b = 16 * u, j = __umulhi(b, L.magic);
+                __builtin_nontemporal_store(lds16u(lds_raw, j * SB + L.blob_off + (b - j * w), m), dst16 + u);
+            }
+        } else if ((w & 3) == 0) {
+            for (uint32_t d = ct; d < D; d += NCT) {
+                const uint32_t b = 4 * d;
+                const uint32_t j = __umulhi(b, L.magic);
+                const uint32_t a = j * SB + L.blob_off + (b - j * w);
+                __builtin_nontemporal_store(lds_bytes4(lds, a), dst + d);
+            }
+        } else if (w == 2) {   // a dword = rows 2d, 2d+1
+            for (uint32_t d = ct; d < D; d += NCT) {
+                const uint32_t a = 2 * d * SB + L.blob_off;
+                const uint32_t x = (lds_bytes4(lds, a) & 0xFFFFu) | (lds_bytes4(lds, a + SB) << 16);
+                __builtin_nontemporal_store(x, dst + d);
+            }
+        } else if (w > 4 && !(L.flags & 1u)) {   // most dwords sit inside one row
+            for (uint32_t d = ct; d < D; d += NCT) {
+                const uint32_t b = 4 * d;
+                const uint32_t j = __umulhi(b, L.magic);
+                const uint32_t r = b - j * w;
+                uint32_t x;
+                if (r + 4 <= w) {
+                    x = lds_bytes4(lds, j * SB + L.blob_off + r);
+                } else {
+                    const uint32_t k = w - r;   // 1..3 bytes of row j, then row j + 1
+                    x = (lds_bytes4(lds, j * SB + L.blob_off + r) & ((1u << (8 * k)) - 1u)) |
+                        (lds_bytes4(lds, (j + 1) * SB + L.blob_off) << (8 * k));
+                }
+                __builtin_nontemporal_store(x, dst + d);
+            }
+        } else {
+            for (uint32_t d = ct; d < D; d += NCT) {
+                uint32_t x = 0;
+#pragma unroll
+                for (int y = 0; y < 4; y++) {
+                    const uint32_t b = 4 * d + y;
+                    const uint32_t j = w > 1 ? __umulhi(b, L.magic) : b;
+                    uint32_t v = lds_u8(lds, j * SB + L.blob_off + (b - j * w));
+                    if (L.flags & 1u) v = v != 0;
+                    x |= v << (8 * y);
+                }
+                __builtin_nontemporal_store(x, dst + d);
+            }
+        }
+        // ragged tail (R % 4 bytes, last tile only)
+        for (uint32_t b = 4 * D + ct; b < R; b += NCT) {
+            const uint32_t j = w > 1 ? __umulhi(b, L.magic) : b;
+            uint32_t v = lds_u8(lds, j * SB + L.blob_off + (b - j * w));
+            if (L.flags & 1u) v = v != 0;
+            L.dst[blob0 * w + b] = (uint8_t)v;
+        }
+    }
+    // 4. validity (every node is present in the canonical layout)
+    for (int c = 0; c < F.n_all_cols; c++)
+        if (cols.valid[c])
+            for (uint32_t j = ct; j < rows; j += NCT) cols.valid[c][blob0 + j] = 1;
+}
+
+template <bool EXT, int NCT>
+__device__ __forceinline__ void dfix_status(const DecProgram& P, const DecCols& cols, const uint8_t* arena,
+                                            const uint64_t* offs, uint32_t B, uint32_t* status, uint32_t* fail,
+                                            uint64_t blob0, uint32_t rows, uint32_t ct, bool clear) {
+    for (uint32_t j = ct; j < rows; j += NCT) {
+        const uint64_t i = blob0 + j;
+        uint32_t sv = 0;
+        const bool f = fail[j] != 0;
+        if (clear) fail[j] = 0;
+        if (f)
+            sv = decode_blob<GReader, EXT>(P, cols, GReader{arena}, offs ? offs[i] : i * B,
+                                           offs ? offs[i + 1] : (i + 1) * B, i);
+#ifdef PACKOS_DEC_STNT
+        __builtin_nontemporal_store(sv, status + i);
+#else
+        status[i] = sv;
+#endif
+    }
+}
+
 template <bool EXT>
-__global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecFixProgram F, DecProgram P, DecCols cols, DecColsK K,
-                                                         const uint8_t* __restrict__ arena,
-                                                         const uint64_t* __restrict__ offs, uint64_t n,
-                                                         uint32_t* __restrict__ status) {
+__device__ __forceinline__ void dfix_oneshot(const DecFixProgram& F, const DecProgram& P, const DecCols& cols,
+                                             const DecColsK& K, const uint8_t* __restrict__ arena,
+                                             const uint64_t* __restrict__ offs, uint64_t n,
+                                             uint32_t* __restrict__ status, uint64_t tile0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
     uint32_t* lds = (uint32_t*)lds_raw;
     const uint32_t B = (uint32_t)F.B, T = (uint32_t)F.T, QW = (B + 3) >> 2;
     // staged row stride (rows padded to B + 16 measured slower: M decode 0.0997
     // -> 0.112 ms with 2.6x fewer bank-conflict cycles; round-4 A/B)
     const uint32_t SB = B;
-    const uint64_t blob0 = (uint64_t)blockIdx.x * T;
+    const uint64_t blob0 = (tile0 + blockIdx.x) * T;
     const uint32_t rows = (uint32_t)min((uint64_t)T, n - blob0);
     const int tid = threadIdx.x;
     uint32_t* chk = lds + (T * SB / 4 + 4);
@@ -1339,123 +1480,124 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecF
         }
         return;
     }
-    // 2. constant-byte check, over the blob dwords that HOLD constant bytes
-    //    (header words, literals: 5 of 64 for metric M; list built at compile)
-    {
-        const uint32_t nq = (uint32_t)F.n_chk;
-        const uint32_t nq_magic = nq > 1 ? (uint32_t)((0x100000000ull + nq - 1) / nq) : 0u;
-        for (uint32_t e = tid; e < rows * nq; e += kBlock) {
-            const uint32_t j = nq > 1 ? __umulhi(e, nq_magic) : e;
-            const uint32_t* c = chk + 3 * (e - j * nq);
-            const uint32_t a = j * SB + 4 * c[0];   // blob dword q (B % 4 == 0: aligned)
-            const uint32_t v = (B & 3) == 0 ? lds[a >> 2] : lds_bytes4(lds, a);
-            if ((v & c[1]) != c[2]) fail[j] = 1;
-        }
-    }
-    // 2b. value checks of fixed leaves (Range, Prefix/Suffix of fixed strings):
-    //    a failing row takes the exact per-blob path, which reports it
-    for (uint32_t e = tid; e < rows * (uint32_t)F.n_vchk; e += kBlock) {
-        const uint32_t j = e / (uint32_t)F.n_vchk;
-        const DecChk c = F.vchk[e - j * (uint32_t)F.n_vchk];
-        const uint32_t a = j * SB + c.blob_off;
-        bool bad;
-        if (c.flags & CHK_RANGE) {
-            uint64_t u = 0;
-            for (uint32_t b = 0; b < c.width; b++) u |= (uint64_t)lds_u8(lds, a + b) << (8 * b);
-            const int sh = 64 - 8 * (int)c.width;
-            const int64_t v = (int64_t)(u << sh) >> sh;
-            bad = ((c.flags & CHK_MIN) && v < c.rmin) || ((c.flags & CHK_MAX) && v > c.rmax);
-        } else {
-            bad = c.lit_len > c.width;
-            const uint32_t at = (c.flags & CHK_PREFIX) ? 0u : c.width - c.lit_len;
-            for (uint32_t b = 0; !bad && b < c.lit_len; b++) bad = lds_u8(lds, a + at + b) != P.lits[c.lit + b];
-        }
-        if (bad) fail[j] = 1;
-    }
-    // 3. columns: uniform walk over the columns; threads stride the column's
-    //    output dwords (consecutive lanes -> consecutive dwords: 256-B stores)
-    for (int c = 0; c < K.n; c++) {
-        struct { uint8_t* dst; uint32_t blob_off, flags, magic; } L = {K.dst[c], K.blob_off[c], K.flags[c], K.magic[c]};
-        const uint32_t w = K.width[c], R = rows * w, D = R >> 2;
-        uint32_t* dst = (uint32_t*)(L.dst + blob0 * w);   // 4-B aligned: T*w % 4 == 0, base 16-B aligned
-        if ((w & 15) == 0 && (SB & 15) == 0 && !(L.flags & 3u)) {   // flags bit 1: PACKOS_DEC_W16=0
-            // 16-B units (a string / bytes column of 16k bytes): a unit lies inside
-            // one row, at the same offset mod 16 in every row (SB % 16 == 0), so
-            // two ds_read_b128 + a shift chosen by a scalar branch per unit and one
-            // 1-KiB-per-wave NT store: a quarter of the dword path's iterations
-            typedef __attribute__((address_space(1))) u32x4 g_v4;
-            g_v4* dst16 = (g_v4*)(L.dst + blob0 * w);
-            const uint32_t U = R >> 4, m = L.blob_off & 15u;
-            for (uint32_t u = tid; u < U; u += kBlock) {
-                const uint32_t b = 16 * u, j = __umulhi(b, L.magic);
-                __builtin_nontemporal_store(lds16u(lds_raw, j * SB + L.blob_off + (b - j * w), m), dst16 + u);
-            }
-        } else if ((w & 3) == 0) {
-            for (uint32_t d = tid; d < D; d += kBlock) {
-                const uint32_t b = 4 * d;
-                const uint32_t j = __umulhi(b, L.magic);
-                const uint32_t a = j * SB + L.blob_off + (b - j * w);
-                __builtin_nontemporal_store(lds_bytes4(lds, a), dst + d);
-            }
-        } else if (w == 2) {   // a dword = rows 2d, 2d+1
-            for (uint32_t d = tid; d < D; d += kBlock) {
-                const uint32_t a = 2 * d * SB + L.blob_off;
-                const uint32_t x = (lds_bytes4(lds, a) & 0xFFFFu) | (lds_bytes4(lds, a + SB) << 16);
-                __builtin_nontemporal_store(x, dst + d);
-            }
-        } else if (w > 4 && !(L.flags & 1u)) {   // most dwords sit inside one row
-            for (uint32_t d = tid; d < D; d += kBlock) {
-                const uint32_t b = 4 * d;
-                const uint32_t j = __umulhi(b, L.magic);
-                const uint32_t r = b - j * w;
-                uint32_t x;
-                if (r + 4 <= w) {
-                    x = lds_bytes4(lds, j * SB + L.blob_off + r);
-                } else {
-                    const uint32_t k = w - r;   // 1..3 bytes of row j, then row j + 1
-                    x = (lds_bytes4(lds, j * SB + L.blob_off + r) & ((1u << (8 * k)) - 1u)) |
-                        (lds_bytes4(lds, (j + 1) * SB + L.blob_off) << (8 * k));
-                }
-                __builtin_nontemporal_store(x, dst + d);
-            }
-        } else {
-            for (uint32_t d = tid; d < D; d += kBlock) {
-                uint32_t x = 0;
-#pragma unroll
-                for (int y = 0; y < 4; y++) {
-                    const uint32_t b = 4 * d + y;
-                    const uint32_t j = w > 1 ? __umulhi(b, L.magic) : b;
-                    uint32_t v = lds_u8(lds, j * SB + L.blob_off + (b - j * w));
-                    if (L.flags & 1u) v = v != 0;
-                    x |= v << (8 * y);
-                }
-                __builtin_nontemporal_store(x, dst + d);
-            }
-        }
-        // ragged tail (R % 4 bytes, last tile only)
-        for (uint32_t b = 4 * D + tid; b < R; b += kBlock) {
-            const uint32_t j = w > 1 ? __umulhi(b, L.magic) : b;
-            uint32_t v = lds_u8(lds, j * SB + L.blob_off + (b - j * w));
-            if (L.flags & 1u) v = v != 0;
-            L.dst[blob0 * w + b] = (uint8_t)v;
-        }
-    }
-    // 4. validity (every node is present in the canonical layout)
-    for (int c = 0; c < F.n_all_cols; c++)
-        if (cols.valid[c])
-            for (uint32_t j = tid; j < rows; j += kBlock) cols.valid[c][blob0 + j] = 1;
+    dfix_tile<kBlock>(F, P, cols, K, lds_raw, chk, fail, blob0, rows, (uint32_t)tid);
     __syncthreads();
-    for (uint32_t j = tid; j < rows; j += kBlock) {
-        const uint64_t i = blob0 + j;
-        uint32_t sv = 0;
-        if (fail[j])
-            sv = decode_blob<GReader, EXT>(P, cols, GReader{arena}, offs ? offs[i] : i * B,
-                                           offs ? offs[i + 1] : (i + 1) * B, i);
-#ifdef PACKOS_DEC_STNT
-        __builtin_nontemporal_store(sv, status + i);
-#else
-        status[i] = sv;
+    dfix_status<EXT, kBlock>(P, cols, arena, offs, B, status, fail, blob0, rows, (uint32_t)tid, false);
+}
+
+template <bool EXT>
+__global__ __launch_bounds__(kBlock) PACKOS_DECFIX_ATTR void k_decode_fixed(DecFixProgram F, DecProgram P, DecCols cols,
+                                                                            DecColsK K, const uint8_t* __restrict__ arena,
+                                                                            const uint64_t* __restrict__ offs, uint64_t n,
+                                                                            uint32_t* __restrict__ status, uint64_t tile0) {
+    dfix_oneshot<EXT>(F, P, cols, K, arena, offs, n, status, tile0);
+}
+// the same at 8 waves per SIMD (64 VGPRs), for blobs under 128 B: their
+// 16-KB tiles leave LDS for 9 workgroups per CU, and the one-shot tile's
+// fixed latency is what small blobs pay for (C2 decode 0.0315 -> 0.0298 ms;
+// M and C4, held to 6 workgroups by their 24-KB tiles, do not gain)
+template <bool EXT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_decode_fixed8(
+    DecFixProgram F, DecProgram P, DecCols cols, DecColsK K, const uint8_t* __restrict__ arena,
+    const uint64_t* __restrict__ offs, uint64_t n, uint32_t* __restrict__ status, uint64_t tile0) {
+    dfix_oneshot<EXT>(F, P, cols, K, arena, offs, n, status, tile0);
+}
+
+// Persistent form (full tiles only; opt-in, PACKOS_DEC_PERSIST): one
+// workgroup walks tiles blockIdx.x, + gridDim.x, ... with two LDS tile
+// buffers.  Wave 0 is the producer: it issues tile k + 1's staging DMA (and
+// the DMA of its offsets) while waves 1..7 write tile k's columns, so the HBM
+// round trip of a tile's rows no longer sits in front of every tile's
+// stores.  The producer issues nothing but DMA, so its vmcnt(0) waits for
+// exactly the tile it needs; the consumer waves never wait on their stores.
+// Measured slower (round 4, same box): M decode 0.098 -> 0.157 ms, C2 0.0315
+// -> 0.052, C4 0.42 -> 0.59.  A tile's column phase, not its load, is the
+// long pole (~11 us per tile either way), and three 8-wave workgroups per CU
+// write half as many tiles at once as six one-shot workgroups.
+constexpr int kDecPBlock = 512, kDecPCons = kDecPBlock - kWave;
+#ifndef PACKOS_DECFIXP_ATTR
+// <= 80 VGPRs: three 8-wave workgroups per CU (the 2 x 24-KB buffers admit three)
+#define PACKOS_DECFIXP_ATTR __attribute__((amdgpu_waves_per_eu(6, 8)))
 #endif
+template <bool EXT>
+__global__ __launch_bounds__(kDecPBlock) PACKOS_DECFIXP_ATTR void k_decode_fixed_p(
+    DecFixProgram F, DecProgram P, DecCols cols, DecColsK K, const uint8_t* __restrict__ arena,
+    const uint64_t* __restrict__ offs, uint64_t ntiles, uint32_t* __restrict__ status) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
+    const uint32_t B = (uint32_t)F.B, T = (uint32_t)F.T, QW = (B + 3) >> 2;
+    const uint32_t TB = T * B;                              // a multiple of 16 (T % 16 == 0)
+    uint64_t* ob = (uint64_t*)(lds_raw + 2 * TB);           // buffer b's offsets at ob + b T
+    uint32_t* chk = (uint32_t*)(ob + 2 * T);
+    uint32_t* fail = chk + 3 * QW;
+    uint32_t* okf = fail + T;                               // okf[b]: buffer b's tile is contiguous
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const bool producer = tid < (uint32_t)kWave;
+    const uint64_t G = gridDim.x;
+    typedef __attribute__((address_space(4))) const uint64_t c_u64;
+    const uint32_t lds0 = (uint32_t)(uintptr_t)lds_raw;
+    // producer: stage tile tt into buffer bb; returns its base offset and
+    // whether its range is the expected aligned T * B bytes (else nothing is
+    // staged and the tile takes the per-blob path)
+    auto issue = [&](uint64_t tt, uint32_t bb, uint64_t& base) -> bool {
+        const uint64_t blob0 = tt * T;
+        base = blob0 * B;
+        uint64_t end = base + TB;
+        if (offs) {
+            base = ((c_u64*)(uintptr_t)offs)[blob0];
+            end = ((c_u64*)(uintptr_t)offs)[blob0 + T];
+        }
+        const bool okp = (base & 15) == 0 && end >= base && end - base == TB;
+        if (okp) {
+            const uint8_t* src = arena + base;
+            const uint32_t lb = lds0 + bb * TB;
+            for (uint32_t c0 = 0; c0 < TB / 16; c0 += kWave)
+                if (c0 + lane < TB / 16) dma16nt(src + 16u * (c0 + lane), __builtin_amdgcn_readfirstlane(lb + 16u * c0));
+            if (offs) {   // offs[blob0 .. blob0 + T) (16-B aligned: host check, T % 16 == 0)
+                const uint8_t* os = (const uint8_t*)(offs + blob0);
+                const uint32_t lo = (uint32_t)(uintptr_t)(ob + bb * T);
+                for (uint32_t c0 = 0; c0 < T / 2; c0 += kWave)
+                    if (c0 + lane < T / 2) dma16(os + 16u * (c0 + lane), __builtin_amdgcn_readfirstlane(lo + 16u * c0));
+            }
+        }
+        return okp;
+    };
+    uint64_t t = blockIdx.x, cur_base = 0;
+    bool cur_okp = false;
+    if (producer && t < ntiles) cur_okp = issue(t, 0, cur_base);
+    // the check table (its load queues behind the first tile's DMA)
+    const uint32_t nchk = 3u * (uint32_t)F.n_chk;
+    for (uint32_t q = tid; q < nchk; q += kDecPBlock) chk[q] = F.chk[q];
+    for (uint32_t j = tid; j < T; j += kDecPBlock) fail[j] = 0;
+    for (uint32_t k = 0; t < ntiles; k++, t += G) {
+        const uint32_t b = k & 1;
+        if (producer) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t's rows and offsets
+            bool ok = cur_okp;
+            if (ok && offs)
+                for (uint32_t j = lane; j < T; j += kWave) ok &= ob[b * T + j] == cur_base + (uint64_t)j * B;
+            ok = __builtin_amdgcn_ballot_w64(!ok) == 0;   // wave-wide AND (every lane active)
+            if (lane == 0) okf[b] = ok ? 1u : 0u;
+        }
+        __syncthreads();   // buffer b staged, okf[b] set; buffer b ^ 1 free
+        const bool ok = okf[b] != 0;
+        const uint64_t blob0 = t * T;
+        if (producer) {
+            if (t + G < ntiles) cur_okp = issue(t + G, b ^ 1, cur_base);
+        } else if (ok) {
+            dfix_tile<kDecPCons>(F, P, cols, K, lds_raw + b * TB, chk, fail, blob0, T, tid - kWave);
+        }
+        __syncthreads();   // fail flags of tile t set; buffer b read
+        if (!producer) {
+            if (ok) {
+                dfix_status<EXT, kDecPCons>(P, cols, arena, offs, B, status, fail, blob0, T, tid - kWave, true);
+            } else {
+                for (uint32_t j = tid - kWave; j < T; j += kDecPCons) {
+                    const uint64_t i = blob0 + j;
+                    status[i] = decode_blob<GReader, EXT>(P, cols, GReader{arena}, offs ? offs[i] : i * B,
+                                                          offs ? offs[i + 1] : (i + 1) * B, i);
+                }
+            }
+        }
     }
 }
 
@@ -1842,6 +1984,34 @@ int current_device(int* dev) {
     }
     HIP_TRY(hipGetDevice(dev));
     return PACKOS_OK;
+}
+
+// compute units of device dev (cached; 256 on MI355X)
+int num_cus(int dev) {
+    static std::mutex mu;
+    static std::map<int, int> cache;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(dev);
+    if (it != cache.end()) return it->second;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 1;
+    cache[dev] = cus;
+    return cus;
+}
+
+// resident workgroups per CU of a kernel at (block, dynamic LDS) (cached)
+template <typename K>
+int occupancy(K kern, int block, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::pair<const void*, size_t>, int> cache;
+    std::lock_guard<std::mutex> g(mu);
+    const auto key = std::make_pair((const void*)kern, lds);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, block, lds) != hipSuccess || nb <= 0) nb = 1;
+    cache[key] = nb;
+    return nb;
 }
 
 
@@ -2449,12 +2619,29 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
             K.flags[c] = f.flags | (s->tune.dec_w16 ? 0u : 2u);
             K.magic[c] = f.magic;
         }
-        if (s->ext)
-            hipLaunchKernelGGL(k_decode_fixed<true>, dim3((unsigned)((n + T - 1) / T)), dim3(kBlock), lds, st, F,
-                               t->dec, dc, K, arena, offsets, (uint64_t)n, status);
-        else
-            hipLaunchKernelGGL(k_decode_fixed<false>, dim3((unsigned)((n + T - 1) / T)), dim3(kBlock), lds, st, F,
-                               t->dec, dc, K, arena, offsets, (uint64_t)n, status);
+        // persistent double-buffered workgroups over the full tiles (offsets
+        // staged by DMA: 16-B aligned), the last partial tile one-shot
+        uint64_t full = n / T, tile0 = 0;
+        const bool persist = ((uintptr_t)offsets & 15) == 0 && full > 0 &&
+                             (s->tune.dec_persist == 2 || (s->tune.dec_persist == 1 && full >= 2 * (uint64_t)num_cus(dev)));
+        if (persist) {
+            const size_t lp = 2 * (size_t)T * B + 16 * (size_t)T + 12 * QW + 4 * (size_t)T + 16;
+            auto kp = s->ext ? k_decode_fixed_p<true> : k_decode_fixed_p<false>;
+            uint64_t slots = (uint64_t)num_cus(dev) * (uint64_t)occupancy(kp, kDecPBlock, lp);
+            if (s->tune.dec_persist_grid > 0) slots = std::min<uint64_t>(slots, (uint64_t)s->tune.dec_persist_grid);
+            const uint64_t per = (full + slots - 1) / slots;   // tiles per workgroup
+            const uint64_t G = (full + per - 1) / per;
+            hipLaunchKernelGGL(kp, dim3((unsigned)G), dim3(kDecPBlock), lp, st, F, t->dec, dc, K, arena, offsets, full,
+                               status);
+            tile0 = full;
+        }
+        const uint64_t rest = (n + T - 1) / T - tile0;
+        if (rest) {
+            auto k1 = B < 128 ? (s->ext ? k_decode_fixed8<true> : k_decode_fixed8<false>)
+                              : (s->ext ? k_decode_fixed<true> : k_decode_fixed<false>);
+            hipLaunchKernelGGL(k1, dim3((unsigned)rest), dim3(kBlock), lds, st, F, t->dec, dc, K, arena, offsets,
+                               (uint64_t)n, status, tile0);
+        }
     } else {
         const size_t ptab = ((s->dnodes.size() * sizeof(DecNode) + 15) & ~(size_t)15) +
                             ((s->dkids.size() * 4 + 15) & ~(size_t)15) + s->lits.size() + 16;
