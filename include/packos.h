@@ -13,8 +13,10 @@
  *                             schema.EncodeValue / EncodeValueNamed (MODE_PUTACCESS) schema/schema.go:912,968
  *                             packable.Pack(args...)        (MODE_PACKABLE)    packable/pack.go:59
  *   packos_encoded_size_batch <- PutAccess.PackSize / Tuple.ValueSize      access/put.go:655, packable/pack.go:17
- *   packos_decode_batch    <- schema.DecodeBuffer / DecodeBufferNamed / ValidateBuffer
- *                             over access.SeqGetAccess                  schema/schema.go:880,893,948; access/seqget.go
+ *   packos_decode_batch    <- schema.DecodeBuffer / DecodeBufferNamed
+ *                             over access.SeqGetAccess                  schema/schema.go:893,948; access/seqget.go
+ *   packos_validate_batch  <- schema.ValidateBuffer (the Validate methods'  schema/schema.go:880
+ *                             rules, which differ from Decode's: see below)
  *   packos_get_field_batch <- access.GetAccess Get*(pos) / GetNestedGetAccess  access/get.go:19-375,492
  *   packos_get_batch          + GetInt / GetFloating / GetTypeAndValue      access/get.go:120-170,504-536
  *   packos_get_map_batch   <- GetMapStr / GetMapAny / GetMapOrderedAny       access/get.go:412-490
@@ -40,7 +42,7 @@
 extern "C" {
 #endif
 
-#define PACKOS_ABI_VERSION 3
+#define PACKOS_ABI_VERSION 4   /* 4: packos_validate_* */
 
 /* ---- return codes (library-level errors) -------------------------------- */
 #define PACKOS_OK              0
@@ -109,8 +111,9 @@ extern "C" {
 #define PACKOS_KIND_MAP     8   /* nested map:   column carries only `valid` */
 
 /* ---- per-blob status word -------------------------------------------------
- * bits 0..7   schema ErrorCode of the error DecodeBuffer/ValidateBuffer would
- *             return (schema/schema.go:24-41); 0 = ok
+ * bits 0..7   schema ErrorCode of the error DecodeBuffer (packos_decode_batch)
+ *             or ValidateBuffer (packos_validate_batch) would return
+ *             (schema/schema.go:24-41); 0 = ok
  * bits 8..23  top-level field position of that error + 1 (0 = position -1)
  * bits 24..29 encode only: the ErrorCode of the leaf error that EncodeValue
  *             wraps in ErrEncode (schema.go:919-936), e.g. ErrOutOfRange for
@@ -196,7 +199,9 @@ typedef struct packos_schema packos_schema;
  * (SchemaNamedChain).  Supported node types: bool, int8..int64,
  * uint8..uint64, float32, float64, string (width / nullable / exact),
  * bytes (width), tuple (schema, fieldNames, nullable, variableLength),
- * map (schema = key,value,... ; keys with "exact" become constants;
+ * map (schema = key,value,... ; keys with "exact" become constants; an
+ * odd schema count compiles: a present value then fails encode and decode
+ * with ErrConstraintViolated (schema.go:369-377, 422-429), as SMap does;
  * "sorted": true sorts the pairs by key bytes at compile time, which is
  * PackMapSorted / AddMapSortedKey order).
  * Value checks, as BuildSchema builds them:
@@ -310,12 +315,15 @@ int packos_encode_batch(const packos_schema* s, const packos_column* cols, size_
 typedef struct packos_pipeline packos_pipeline;
 int  packos_pipeline_create(const packos_schema* s, size_t chunk_blobs, int slots, packos_pipeline** out);
 void packos_pipeline_free(packos_pipeline* p);
-/* packos_encode_host_batch / packos_decode_host_batch on an explicit
- * pipeline (same arguments and results; chunking from the pipeline)        */
+/* packos_encode_host_batch / packos_decode_host_batch /
+ * packos_validate_host_batch on an explicit pipeline (same arguments and
+ * results; chunking from the pipeline)                                      */
 int  packos_pipeline_encode(packos_pipeline* p, const packos_column* host_cols, size_t n_blobs, uint8_t* host_out,
                             uint64_t out_capacity, uint64_t* host_offsets, uint32_t* host_status);
 int  packos_pipeline_decode(packos_pipeline* p, const uint8_t* host_arena, const uint64_t* host_offsets,
                             uint64_t stride, size_t n_blobs, packos_column* host_cols, uint32_t* host_status);
+int  packos_pipeline_validate(packos_pipeline* p, const uint8_t* host_arena, const uint64_t* host_offsets,
+                              uint64_t stride, size_t n_blobs, uint32_t* host_status);
 
 /* Encode n blobs whose columns live in HOST memory into a host arena — the
  * entry point a cgo / JNI shim calls for RPC payloads or BadgerDB values
@@ -352,6 +360,12 @@ int packos_decode_host_batch(const packos_schema* s, const uint8_t* host_arena, 
                              uint64_t stride, size_t n_blobs, packos_column* host_cols, uint32_t* host_status,
                              size_t chunk_blobs);
 
+/* ValidateBuffer over a HOST arena (schema/schema.go:880-891): chunks go H2D
+ * like packos_decode_host_batch, through packos_validate_batch, and only the
+ * status comes back.  host_status (n) is required.  Blocks until done.     */
+int packos_validate_host_batch(const packos_schema* s, const uint8_t* host_arena, const uint64_t* host_offsets,
+                               uint64_t stride, size_t n_blobs, uint32_t* host_status, size_t chunk_blobs);
+
 /* ---- batch decode (schema.DecodeBuffer semantics) ------------------------- */
 
 /* blob i = arena[offsets[i] .. offsets[i+1]); offsets == NULL means fixed
@@ -361,6 +375,26 @@ int packos_decode_host_batch(const packos_schema* s, const uint8_t* host_arena, 
 int packos_decode_batch(const packos_schema* s, const uint8_t* arena, const uint64_t* offsets,
                         uint64_t stride, size_t n_blobs, packos_column* out_cols,
                         uint32_t* status, void* stream);
+
+/* ---- batch validate (schema.ValidateBuffer semantics) --------------------- */
+
+/* status[i] = the error ValidateBuffer(blob i, chain) would return, in the
+ * status-word layout above (a ValidateBuffer panic sets bit 30).  No columns.
+ * ValidateBuffer runs each schema's Validate method, whose rules differ from
+ * Decode's (packos_decode_batch) in three places of the compiled subset:
+ *   - a nullable bool / int / uint / float leaf never reads its payload
+ *     (validatePrimitive, schema.go:596-715): a payload shorter than the type
+ *     passes, where Decode panics; Range / date leaves read it either way
+ *     (:1177-1188, :2198-2212)
+ *   - a prefix / suffix / exact string check of a nullable string (width <= 0)
+ *     passes an empty value (after the decodeDefault substitution) without
+ *     testing it (CheckFunc ValidateFunc, :1085-1087); Decode tests it
+ *   - a map with an odd schema count validates its schemas in sequence
+ *     (SchemaMap.Validate, :336-359); Decode fails ErrConstraintViolated
+ * A blob DecodeBuffer accepts is always accepted here.  blob i =
+ * arena[offsets[i] .. offsets[i+1]) or the `stride`-byte slot i.           */
+int packos_validate_batch(const packos_schema* s, const uint8_t* arena, const uint64_t* offsets,
+                          uint64_t stride, size_t n_blobs, uint32_t* status, void* stream);
 
 /* ---- random-access gather (GetAccess semantics) --------------------------- */
 

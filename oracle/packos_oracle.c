@@ -419,8 +419,10 @@ int64_t or_encoded_size_one(const or_schema* s, const packos_column* cols, size_
  * 444-449).  Nil containers and nil values are not encoded, so not checked
  * (schema.go:1203-1214, 2227-2246, 1110-1124, 1804-1806).                    */
 static int has_names_bad(const or_schema* s) {
-    for (int n = 0; n < s->n_nodes; n++)
+    for (int n = 0; n < s->n_nodes; n++) {
         if (NK(s, n) == ORN_TUPLE && (NC(s, n) & ORT_NAMES_BAD)) return 1;
+        if (NK(s, n) == ORN_MAP && (NB(s, n) % 2) != 0) return 1;   /* odd SMap */
+    }
     return 0;
 }
 
@@ -432,6 +434,9 @@ static int enc_check(const or_schema* s, const packos_column* cols, size_t i, in
         if (k == ORN_TUPLE && (NC(s, n) & ORT_NAMES_BAD)) return 3;
         int kids[256];
         int nk = children(s, n, kids);
+        /* SchemaMap.Encode of a present value with an odd schema count:
+         * SizeExact -> ErrConstraintViolated (schema.go:417-429)             */
+        if (k == ORN_MAP && (nk % 2) != 0) return 3;
         for (int j = 0; j < nk; j++) {
             if (enc_check(s, cols, i, kids[j])) return 1;
         }
@@ -682,6 +687,7 @@ int or_seq_peek_nested(const or_seq* s, or_seq* nested) {
 typedef struct dec_ctx {
     const or_schema* s; packos_column* cols; size_t i; uint64_t blob_base;
     int ext;   /* PACKOS_MODE_EXTENDED: tag-2 fields are extended containers */
+    int val;   /* ValidateBuffer (schema.go:880-891): Validate rules, no outputs */
 } dec_ctx;
 
 #define DEC_PANIC 0x100
@@ -716,13 +722,24 @@ static int prim(or_seq* q, int tag, int64_t hint, int nullable, int64_t* ps, int
 static int dec_node(dec_ctx* c, int n, or_seq* q, uint64_t sub_base) {
     const or_schema* s = c->s;
     int k = NK(s, n);
-    packos_column* col = s->col_of_node[n] >= 0 ? &c->cols[s->col_of_node[n]] : NULL;
+    packos_column* col = !c->val && s->col_of_node[n] >= 0 ? &c->cols[s->col_of_node[n]] : NULL;
     int64_t ps, w;
     switch (k) {
         case ORN_INT: case ORN_UINT: case ORN_FLOAT: case ORN_BOOL: {
             int W = NA(s, n), nul = NB(s, n);
             int e = prim(q, leaf_tag(k), W, nul, &ps, &w);
             if (e) return e;
+            if (c->val) {
+                /* Validate: SBool..SFloat64 only run validatePrimitive, which never
+                 * reads the payload (schema.go:596-715), so a short nullable payload
+                 * passes; Range / SDateRange ValidateFuncs read it like their
+                 * DecodeFuncs (:1177-1188, :2198-2212) and panic alike          */
+                if (ps < 0 || !(xflags(s, n) & (X_MIN | X_MAX | X_DATE))) return 0;
+                if (w < W) return DEC_PANIC;
+                if ((xflags(s, n) & (X_MIN | X_MAX)) && range_bad(s, n, q->buf + ps, W))
+                    return (xflags(s, n) & X_DATE) ? PACKOS_ERR_DATE_OUT_OF_RANGE : PACKOS_ERR_OUT_OF_RANGE;
+                return 0;
+            }
             if (ps < 0) { if (col->valid) col->valid[c->i] = 0; return 0; }
             if (w < W) return DEC_PANIC; /* binary.LittleEndian.UintXX on a short slice panics */
             uint8_t* dst = (uint8_t*)col->data + c->i * (size_t)W;
@@ -741,6 +758,16 @@ static int dec_node(dec_ctx* c, int n, or_seq* q, uint64_t sub_base) {
             size_t have = ps < 0 ? 0 : (size_t)w, dl = 0;
             const uint8_t* dp = (xflags(s, n) & X_DEFAULT) ? xlit(s, n, 1, &dl) : NULL;
             int dflt = have == 0 && dl > 0;   /* DefaultDecodeVal replaces an empty payload */
+            if (c->val) {
+                /* SchemaString/SchemaBytes.Validate = validatePrimitive (schema.go:275-277,
+                 * 304-306); CheckFunc's ValidateFunc passes an empty string of a nullable
+                 * receiver before the test (:1085-1087), the default applied first   */
+                if (!(xflags(s, n) & (X_PREFIX | X_SUFFIX))) return 0;
+                if (W <= 0 && (dflt ? dl : have) == 0) return 0;
+                if (str_bad(s, n, dflt ? dp : q->buf + (ps < 0 ? 0 : ps), dflt ? dl : have))
+                    return (xflags(s, n) & X_PREFIX) ? PACKOS_ERR_STRING_PREFIX : PACKOS_ERR_STRING_SUFFIX;
+                return 0;
+            }
             if (W > 0) {
                 memcpy((uint8_t*)col->data + c->i * (size_t)W, q->buf + ps, (size_t)W);
             } else {
@@ -763,6 +790,7 @@ static int dec_node(dec_ctx* c, int n, or_seq* q, uint64_t sub_base) {
             const uint8_t* dp = (xflags(s, n) & X_DEFAULT) ? xlit(s, n, 1, &dl) : NULL;
             const uint8_t* vp = q->buf + (ps < 0 ? 0 : ps);
             if (have == 0 && dl > 0) { vp = dp; have = dl; }
+            if (c->val && NB(s, n) <= 0 && have == 0) return 0;   /* ValidateFunc (schema.go:1085-1087) */
             if (have != ll || (ll && memcmp(vp, lp, ll) != 0)) return PACKOS_ERR_STRING_MATCH;
             return 0;
         }
@@ -776,7 +804,9 @@ static int dec_node(dec_ctx* c, int n, or_seq* q, uint64_t sub_base) {
             if (e) return e;
             int kids[256];
             int nk = children(s, n, kids);
-            if (k == ORN_MAP && (nk % 2) != 0) return 3; /* SizeExact (schema.go:395-403) */
+            /* SizeExact: Decode only (schema.go:369-377); SchemaMap.Validate has no
+             * such check and validates the schemas in sequence (:336-359)    */
+            if (k == ORN_MAP && (nk % 2) != 0 && !c->val) return 3;
             if (w != 0) {
                 or_seq sub;
                 if (xc) {
@@ -808,14 +838,14 @@ static int dec_node(dec_ctx* c, int n, or_seq* q, uint64_t sub_base) {
 }
 
 static uint32_t decode_one(const or_schema* s, const uint8_t* blob, int64_t len, uint64_t base,
-                           packos_column* cols, size_t i, int ext) {
+                           packos_column* cols, size_t i, int ext, int val) {
     or_seq q;
     if (ext && len >= 2 && rd16(blob) == or_encode_header(0, PACKOS_TAG_EXTENDED)) {
         if (or_seq_init_ext(&q, blob, len, PACKOS_TAG_TUPLE)) return (uint32_t)PACKOS_ERR_INVALID_FORMAT;
     } else if (or_seq_init(&q, blob, len)) {
         return (uint32_t)PACKOS_ERR_INVALID_FORMAT; /* pos -1 */
     }
-    dec_ctx c = {s, cols, i, base, ext};
+    dec_ctx c = {s, cols, i, base, ext, val};
     for (int t = 0; t < s->n_top; t++) {
         int e = dec_node(&c, s->top_nodes[t], &q, base);
         if (e == DEC_PANIC) return PACKOS_STATUS_PANIC | ((uint32_t)(t + 1) << 8);
@@ -827,14 +857,14 @@ static uint32_t decode_one(const or_schema* s, const uint8_t* blob, int64_t len,
 
 typedef struct dec_job {
     const or_schema* s; const uint8_t* arena; const uint64_t* offs; uint64_t stride;
-    packos_column* cols; uint32_t* status; size_t lo, hi; int ext;
+    packos_column* cols; uint32_t* status; size_t lo, hi; int ext, val;
 } dec_job;
 static void* dec_worker(void* arg) {
     dec_job* j = (dec_job*)arg;
     for (size_t i = j->lo; i < j->hi; i++) {
         uint64_t a = j->offs ? j->offs[i] : i * j->stride;
         uint64_t b = j->offs ? j->offs[i + 1] : (i + 1) * j->stride;
-        j->status[i] = decode_one(j->s, j->arena + a, (int64_t)(b - a), a, j->cols, i, j->ext);
+        j->status[i] = decode_one(j->s, j->arena + a, (int64_t)(b - a), a, j->cols, i, j->ext, j->val);
     }
     return NULL;
 }
@@ -842,8 +872,20 @@ int or_decode_batch(const or_schema* s, const uint8_t* arena, const uint64_t* of
                     size_t n, packos_column* cols, uint32_t* status, int nthreads) {
     return or_decode_batch_mode(s, arena, offsets, stride, n, cols, status, nthreads, 0);
 }
+static int dec_run(const or_schema* s, const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
+                   size_t n, packos_column* cols, uint32_t* status, int nthreads, int mode, int val);
 int or_decode_batch_mode(const or_schema* s, const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
                          size_t n, packos_column* cols, uint32_t* status, int nthreads, int mode) {
+    return dec_run(s, arena, offsets, stride, n, cols, status, nthreads, mode, 0);
+}
+/* ValidateBuffer (schema/schema.go:880-891) per blob: the status word
+ * DecodeBuffer's would be under the Validate methods' rules (no outputs)    */
+int or_validate_batch(const or_schema* s, const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
+                      size_t n, uint32_t* status, int nthreads, int mode) {
+    return dec_run(s, arena, offsets, stride, n, NULL, status, nthreads, mode, 1);
+}
+static int dec_run(const or_schema* s, const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
+                   size_t n, packos_column* cols, uint32_t* status, int nthreads, int mode, int val) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > OR_MAX_THREADS) nthreads = OR_MAX_THREADS;
     pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
@@ -852,7 +894,7 @@ int or_decode_batch_mode(const or_schema* s, const uint8_t* arena, const uint64_
     for (int t = 0; t < nthreads; t++) {
         size_t lo = (size_t)t * per, hi = lo + per > n ? n : lo + per;
         if (lo > hi) lo = hi;
-        dj[t] = (dec_job){s, arena, offsets, stride, cols, status, lo, hi, (mode & PACKOS_MODE_EXTENDED) != 0};
+        dj[t] = (dec_job){s, arena, offsets, stride, cols, status, lo, hi, (mode & PACKOS_MODE_EXTENDED) != 0, val};
         pthread_create(&th[t], NULL, dec_worker, &dj[t]);
     }
     for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);

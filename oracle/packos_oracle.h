@@ -116,6 +116,9 @@ int or_decode_batch(const or_schema* s, const uint8_t* arena, const uint64_t* of
 int or_decode_batch_mode(const or_schema* s, const uint8_t* arena, const uint64_t* offsets,
                          uint64_t stride, size_t n, packos_column* out_cols, uint32_t* status,
                          int nthreads, int mode);
+/* ValidateBuffer (schema/schema.go:880-891): status only, Validate rules */
+int or_validate_batch(const or_schema* s, const uint8_t* arena, const uint64_t* offsets,
+                      uint64_t stride, size_t n, uint32_t* status, int nthreads, int mode);
 
 /* ---- SeqGetAccess restatement (access/seqget.go) ---- */
 typedef struct or_seq {

@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PACKOS_LIB") or os.path.join(HERE, "libpackos.so")  # override: experiments only
 
-ABI_VERSION = 3        # PACKOS_ABI_VERSION this binding's structs and signatures follow
+ABI_VERSION = 4        # PACKOS_ABI_VERSION this binding's structs and signatures follow
 MODE_PUTACCESS = 0
 MODE_PACKABLE = 1
 MODE_EXTENDED = 0x100   # ADR-001 extended containers (include/packos.h), OR-ed into a mode
@@ -38,6 +38,7 @@ EXPORTED = [
     "packos_schema_describe", "packos_schema_blob_size_host", "packos_encode_workspace_size",
     "packos_encoded_size_batch", "packos_encode_batch", "packos_encode_host_batch", "packos_decode_host_batch", "packos_decode_batch",
     "packos_pipeline_create", "packos_pipeline_free", "packos_pipeline_encode", "packos_pipeline_decode",
+    "packos_pipeline_validate", "packos_validate_batch", "packos_validate_host_batch",
     "packos_get_field_batch", "packos_get_batch", "packos_get_map_batch", "packos_strerror", "packos_last_error", "packos_abi_version",
     "packos_last_encoder",
 ]
@@ -109,6 +110,9 @@ def lib():
     L.packos_pipeline_encode.argtypes = [vp, C.POINTER(PackosColumn), sz, vp, u64, vp, vp]
     L.packos_pipeline_decode.argtypes = [vp, vp, vp, u64, sz, C.POINTER(PackosColumn), vp]
     L.packos_decode_batch.argtypes = [vp, vp, vp, u64, sz, C.POINTER(PackosColumn), vp, vp]
+    L.packos_validate_batch.argtypes = [vp, vp, vp, u64, sz, vp, vp]
+    L.packos_validate_host_batch.argtypes = [vp, vp, vp, u64, sz, vp, sz]
+    L.packos_pipeline_validate.argtypes = [vp, vp, vp, u64, sz, vp]
     L.packos_get_field_batch.argtypes = [vp, vp, u64, sz, C.POINTER(C.c_int32), i32, i32, i32,
                                          vp, vp, vp, vp, vp]
     L.packos_get_batch.argtypes = [vp, vp, u64, sz, C.POINTER(C.c_int32), i32, i32, i32, i32,

@@ -328,6 +328,17 @@ class Pipeline:
                                            st.ctypes.data), "packos_pipeline_decode")
         return out, st[:n]
 
+    def validate(self, arena: np.ndarray, offsets: Optional[np.ndarray], n: int, stride: int = 0,
+                 status: Optional[np.ndarray] = None):
+        """packos_pipeline_validate: the status like validate_host_batch."""
+        a = np.ascontiguousarray(arena, dtype=np.uint8)
+        o = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+        st = status if status is not None else np.empty(max(n, 1), np.uint32)
+        check(lib().packos_pipeline_validate(self._h, a.ctypes.data if a.size else None,
+                                             None if o is None else o.ctypes.data, stride, n, st.ctypes.data),
+              "packos_pipeline_validate")
+        return st[:n]
+
 
 class HostDecoded:
     """Host (numpy) decode output of decode_host_batch, the layout of
@@ -485,6 +496,38 @@ def decode_batch(schema: CompiledSchema, arena, offsets=None, n: Optional[int] =
                                     out.ctypes_array(), status.data_ptr(), _stream_ptr(stream)),
           "packos_decode_batch")
     return out, status[:n]
+
+
+def validate_batch(schema: CompiledSchema, arena, offsets=None, n: Optional[int] = None, stride: int = 0,
+                   stream=None, status=None):
+    """schema.ValidateBuffer over every blob (packos_validate_batch): the int32
+    status word per blob, under the Validate methods' rules
+    (schema/schema.go:880-891; include/packos.h lists where they differ from
+    DecodeBuffer's).  No columns."""
+    torch = _torch()
+    if n is None:
+        n = offsets.numel() - 1
+    if status is None:
+        status = torch.empty(max(n, 1), dtype=torch.int32, device=arena.device)
+    elif status.numel() < n or status.dtype != torch.int32:
+        raise ValueError("validate_batch: `status` needs n int32 entries")
+    check(lib().packos_validate_batch(schema.handle, arena.data_ptr(),
+                                      None if offsets is None else offsets.data_ptr(), stride, n,
+                                      status.data_ptr(), _stream_ptr(stream)), "packos_validate_batch")
+    return status[:n]
+
+
+def validate_host_batch(schema: CompiledSchema, arena: np.ndarray, offsets: Optional[np.ndarray], n: int,
+                        stride: int = 0, chunk_blobs: int = 0, status: Optional[np.ndarray] = None):
+    """ValidateBuffer over a HOST-resident batch (packos_validate_host_batch):
+    the uint32 status per blob."""
+    a = np.ascontiguousarray(arena, dtype=np.uint8)
+    o = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+    st = status if status is not None else np.empty(max(n, 1), np.uint32)
+    check(lib().packos_validate_host_batch(schema.handle, a.ctypes.data if a.size else None,
+                                           None if o is None else o.ctypes.data, stride, n, st.ctypes.data,
+                                           chunk_blobs), "packos_validate_host_batch")
+    return st[:n]
 
 
 def get_field_batch(arena, offsets, n: int, path, want_tag: int, want_width: int, stride: int = 0,

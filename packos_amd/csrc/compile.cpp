@@ -276,8 +276,9 @@ struct Builder {
                 n.sorted = bool_field(j, "sorted");
             }
             if (sch && sch->kind == JVal::ARR) {
-                if (sch->arr.size() % 2)
-                    fail(PACKOS_E_SCHEMA, "map schema needs key,value pairs (schema.go:395-403)");
+                // an odd schema count compiles: Encode fails a present value and
+                // Decode every non-nil map with SizeExact (schema.go:369-377,
+                // 422-429), but Validate has no such check (:336-359)
                 for (size_t k = 0; k < sch->arr.size(); k++) {
                     int kid = node(sch->arr[k], id, depth + 1, top, name);
                     int kk = s->nodes[kid].kind;
@@ -301,6 +302,7 @@ struct Builder {
                 });
                 std::vector<int> k2;
                 for (auto& p : pairs) { k2.push_back(p.first); k2.push_back(p.second); }
+                if (n.kids.size() % 2) k2.push_back(n.kids.back());   // odd count: the unpaired key stays last
                 n.kids = k2;
             }
         } else {
@@ -421,9 +423,10 @@ struct Builder {
                 if (can_nil) s->has_nullable = true;
                 int cid = (int)s->conts.size();
                 s->conts.push_back(c);
-                if (n.kind == K_TUPLE && n.names_bad) {
+                if ((n.kind == K_TUPLE && n.names_bad) || (n.kind == K_MAP && (n.kids.size() & 1))) {
                     // TupleSchemaNamed.Encode of a present value fails before writing
-                    // anything (schema.go:1808-1810); a parent tuple / map wraps it as
+                    // anything (schema.go:1808-1810), so does SchemaMap.Encode with an
+                    // odd schema count (:422-429); a parent tuple / map wraps it as
                     // ErrInvalidFormat
                     EncCheck k{};
                     k.col = n.col;
@@ -968,6 +971,26 @@ int packos_schema_compile(const char* schema_json, int mode, packos_schema** out
             }
             s->dec_prefix = pre;
             s->dec_tail_fixed = tail;
+            // ValidateBuffer reads header words, literals (Match) and the
+            // payloads of Range / date / prefix / suffix leaves only: the bytes
+            // up to the last of those before the first var item, when none
+            // follows it (else the whole window, as decode)
+            int64_t p = 0, need = 0;
+            bool v = false, after = false;
+            for (const EncItem& it : s->items) {
+                bool reads = it.type == IT_HDR || it.type == IT_CONST;
+                if ((it.type == IT_FIXED || it.type == IT_VAR) && it.col >= 0) {
+                    const Node& nd = s->nodes[s->col_node[it.col]];
+                    reads = (nd.check & (CHK_RANGE | CHK_DATE | CHK_STR)) != 0;
+                }
+                if (it.type == IT_VAR) v = true;
+                if (reads && v) after = true;
+                if (!v) {
+                    p += it.size;
+                    if (reads) need = p;
+                }
+            }
+            s->val_win = after || s->ext ? 0 : need;
         }
         b.build_fixed();
         b.build_decode();

@@ -169,7 +169,7 @@ struct packos_pipeline {
     int encode_impl(const packos_column* hc, size_t n, uint8_t* host_out, uint64_t out_capacity,
                     uint64_t* host_offsets, uint32_t* host_status);
     int decode_impl(const uint8_t* host_arena, const uint64_t* host_offsets, uint64_t stride, size_t n,
-                    packos_column* host_cols, uint32_t* host_status);
+                    packos_column* host_cols, uint32_t* host_status, bool val);
     // a failed call still drains its queued work before the buffers are reused
     int encode(const packos_column* hc, size_t n, uint8_t* host_out, uint64_t out_capacity, uint64_t* host_offsets,
                uint32_t* host_status) {
@@ -177,9 +177,10 @@ struct packos_pipeline {
         if (r != PACKOS_OK) drain();
         return r;
     }
+    // val: ValidateBuffer (packos_validate_batch), status only, host_cols unused
     int decode(const uint8_t* host_arena, const uint64_t* host_offsets, uint64_t stride, size_t n,
-               packos_column* host_cols, uint32_t* host_status) {
-        const int r = decode_impl(host_arena, host_offsets, stride, n, host_cols, host_status);
+               packos_column* host_cols, uint32_t* host_status, bool val = false) {
+        const int r = decode_impl(host_arena, host_offsets, stride, n, host_cols, host_status, val);
         if (r != PACKOS_OK) drain();
         return r;
     }
@@ -364,14 +365,14 @@ int packos_pipeline::encode_impl(const packos_column* hc, size_t n, uint8_t* hos
 
 // ------------------------------------------------------------------ decode
 int packos_pipeline::decode_impl(const uint8_t* host_arena, const uint64_t* host_offsets, uint64_t stride, size_t n,
-                            packos_column* host_cols, uint32_t* host_status) {
-    if (!host_cols || !host_status || (!host_arena && n)) {
-        set_error("packos_decode_host_batch: bad argument");
+                            packos_column* host_cols, uint32_t* host_status, bool val) {
+    if ((!host_cols && !val) || !host_status || (!host_arena && n)) {
+        set_error(val ? "packos_validate_host_batch: bad argument" : "packos_decode_host_batch: bad argument");
         return PACKOS_E_INVALID;
     }
     if (n == 0) return PACKOS_OK;
     if (!host_offsets && stride == 0) { set_error("offsets or stride required"); return PACKOS_E_INVALID; }
-    const size_t ncol = s->col_node.size();
+    const size_t ncol = val ? 0 : s->col_node.size();
     const std::vector<ColKind> kind = col_kinds(s);
     std::vector<char> has_valid(ncol, 0);   // the decoder writes validity for these
     for (size_t c = 0; c < ncol; c++) {
@@ -456,7 +457,8 @@ int packos_pipeline::decode_impl(const uint8_t* host_arena, const uint64_t* host
         // biased arena: host byte x is at darena + kPad + (x - a); only
         // offsets inside [a, b) (plus the decoders' 16-B window rounding) are read
         const uint8_t* biased = sl.darena.as<uint8_t>() + kPad - a;
-        HP_RC(packos_decode_batch(s, biased, sl.doffs.as<uint64_t>(), 0, m, dc.data(), sl.dstatus.as<uint32_t>(), comp));
+        if (val) HP_RC(packos_validate_batch(s, biased, sl.doffs.as<uint64_t>(), 0, m, sl.dstatus.as<uint32_t>(), comp));
+        else HP_RC(packos_decode_batch(s, biased, sl.doffs.as<uint64_t>(), 0, m, dc.data(), sl.dstatus.as<uint32_t>(), comp));
         HP_TRY(hipEventRecord(sl.ev_comp, comp));
         HP_TRY(hipStreamWaitEvent(d2h, sl.ev_comp, 0));
         HP_TRY(hipMemcpyAsync(host_status + s0, sl.dstatus.p, m * sizeof(uint32_t), hipMemcpyDeviceToHost, d2h));
@@ -555,6 +557,14 @@ int packos_pipeline_decode(packos_pipeline* p, const uint8_t* host_arena, const 
     return p->decode(host_arena, host_offsets, stride, n, host_cols, host_status);
 }
 
+int packos_pipeline_validate(packos_pipeline* p, const uint8_t* host_arena, const uint64_t* host_offsets,
+                             uint64_t stride, size_t n, uint32_t* host_status) {
+    if (!p) { set_error("packos_pipeline_validate: null pipeline"); return PACKOS_E_INVALID; }
+    std::lock_guard<std::mutex> g(p->mu);
+    DeviceGuard dg(p->device);
+    return p->decode(host_arena, host_offsets, stride, n, nullptr, host_status, true);
+}
+
 int packos_encode_host_batch(const packos_schema* cs, const packos_column* hc, size_t n, uint8_t* host_out,
                              uint64_t out_capacity, uint64_t* host_offsets, uint32_t* host_status, size_t chunk_blobs) {
     if (!cs) { set_error("packos_encode_host_batch: bad argument"); return PACKOS_E_INVALID; }
@@ -570,6 +580,14 @@ int packos_decode_host_batch(const packos_schema* cs, const uint8_t* host_arena,
     PipeLease L;
     HP_RC(lease(const_cast<packos_schema*>(cs), chunk_blobs, L));
     return L.p->decode(host_arena, host_offsets, stride, n, host_cols, host_status);
+}
+
+int packos_validate_host_batch(const packos_schema* cs, const uint8_t* host_arena, const uint64_t* host_offsets,
+                               uint64_t stride, size_t n, uint32_t* host_status, size_t chunk_blobs) {
+    if (!cs) { set_error("packos_validate_host_batch: bad argument"); return PACKOS_E_INVALID; }
+    PipeLease L;
+    HP_RC(lease(const_cast<packos_schema*>(cs), chunk_blobs, L));
+    return L.p->decode(host_arena, host_offsets, stride, n, nullptr, host_status, true);
 }
 
 }  // extern "C"

@@ -772,7 +772,12 @@ struct Frame {
 // the fixed-layout fast path (same code, so the qualification is exact).
 // EXT (PACKOS_MODE_EXTENDED): a top-level blob starting 02 00 and every
 // tag-2 field are read as extended containers (program.h).
-template <class R, bool EXT = false>
+// VAL: ValidateBuffer (schema.go:880-891) instead — the status under the
+// Validate methods' rules, no outputs (cols unused): SBool..SFloat64 never
+// read their payload (:596-715, no short-payload panic), CheckFunc passes an
+// empty string of a nullable receiver (:1085-1087), SchemaMap has no
+// odd-count check (:336-359).
+template <class R, bool EXT = false, bool VAL = false>
 __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& cols, const R& arena, uint64_t a0,
                                          uint64_t a1, uint64_t i) {
     // the current frame lives in registers; outer frames are spilled to `stk`
@@ -791,7 +796,7 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
         if (cur.k >= fn.nkids) {
             if (d == 0) break;
             // container finished: mark it present, then Advance the parent past it
-            if (cols.valid[fn.col]) cols.valid[fn.col][i] = 1;
+            if (!VAL && cols.valid[fn.col]) cols.valid[fn.col][i] = 1;
             d--;
             cur = stk[d];
             const int a = dseq_advance(cur.q, arena);
@@ -808,7 +813,7 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
             const bool xc = EXT && q.cur_type == PACKOS_TAG_EXTENDED;   // an extended container field
             err = dprecheck(q, xc ? PACKOS_TAG_EXTENDED : nd.tag, -1, nd.nullable, w);
             if (err) break;
-            if (nd.kind == K_MAP && (nd.nkids & 1)) { err = 3; break; }
+            if (!VAL && nd.kind == K_MAP && (nd.nkids & 1)) { err = 3; break; }
             if (w != 0) {
                 // PeekNestedSeq (seqget.go:105-121)
                 if (q.next_off - q.cur_off <= 0 || q.next_off > q.len) { err = 1; break; }
@@ -832,7 +837,7 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
                 d++;
                 continue;
             }
-            if (cols.valid[nd.col]) cols.valid[nd.col][i] = 0;  // nil container
+            if (!VAL && cols.valid[nd.col]) cols.valid[nd.col][i] = 0;  // nil container
             const int a = dseq_advance(q, arena);
             if (a) { err = a == 2 ? kPanic : 2; break; }
             cur.k++;
@@ -853,15 +858,22 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
         const bool dflt = have == 0 && (nd.check & CHK_DEFAULT) && nd.dlit_len > 0;
         switch (nd.kind) {
             case K_INT: case K_UINT: case K_FLOAT: case K_BOOL: {
-                if (ps < 0) {
-                    if (cols.valid[nd.col]) cols.valid[nd.col][i] = 0;
-                    break;
+                if (VAL) {
+                    // only Range / SDateRange ValidateFuncs read the payload
+                    // (schema.go:1177-1188, 2198-2212)
+                    if (ps < 0 || !(nd.check & (CHK_RANGE | CHK_DATE))) break;
+                    if (w < nd.width) { err = kPanic; break; }
+                } else {
+                    if (ps < 0) {
+                        if (cols.valid[nd.col]) cols.valid[nd.col][i] = 0;
+                        break;
+                    }
+                    if (w < nd.width) { err = kPanic; break; }  // LittleEndian.UintXX on a short slice
+                    uint8_t* dstp = cols.data[nd.col] + i * (uint64_t)nd.width;
+                    if (nd.kind == K_BOOL) dstp[0] = arena(pay) != 0;
+                    else copy_out(dstp, arena, pay, (uint32_t)nd.width);
+                    if (cols.valid[nd.col]) cols.valid[nd.col][i] = 1;
                 }
-                if (w < nd.width) { err = kPanic; break; }  // LittleEndian.UintXX on a short slice
-                uint8_t* dstp = cols.data[nd.col] + i * (uint64_t)nd.width;
-                if (nd.kind == K_BOOL) dstp[0] = arena(pay) != 0;
-                else copy_out(dstp, arena, pay, (uint32_t)nd.width);
-                if (cols.valid[nd.col]) cols.valid[nd.col][i] = 1;
                 if (nd.check & CHK_RANGE) {   // CheckIntRange after Advance (schema.go:1187-1201, 2213-2224)
                     uint64_t u = 0;
                     for (int b = 0; b < nd.width; b++) u |= (uint64_t)arena(pay + b) << (8 * b);
@@ -873,14 +885,16 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
                 break;
             }
             case K_STRING: case K_BYTES:
-                if (nd.width > 0) {
+                if (VAL) {
+                } else if (nd.width > 0) {
                     uint8_t* dstp = cols.data[nd.col] + i * (uint64_t)nd.width;
                     copy_out(dstp, arena, pay, (uint32_t)nd.width);
                 } else {
                     cols.start[nd.col][i] = dflt ? PACKOS_VIEW_DEFAULT : ps < 0 ? 0ull : q.start + (uint64_t)ps;
                     cols.length[nd.col][i] = dflt ? nd.dlit_len : have;
                 }
-                if (nd.check & CHK_STR) {   // CheckFunc DecodeFunc: HasPrefix / HasSuffix (schema.go:1093-1108)
+                if ((nd.check & CHK_STR) && !(VAL && nd.nullable && (dflt ? nd.dlit_len : have) == 0)) {
+                    // CheckFunc DecodeFunc / ValidateFunc: HasPrefix / HasSuffix (schema.go:1072-1108)
                     const uint32_t len = dflt ? nd.dlit_len : have, L = nd.lit_len;
                     bool ok = len >= L;
                     const uint32_t at = (nd.check & CHK_PREFIX) ? 0u : len - L;
@@ -893,6 +907,7 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
                 break;
             case K_MATCH: {
                 const uint32_t len = dflt ? nd.dlit_len : have;
+                if (VAL && nd.nullable && len == 0) break;   // ValidateFunc (schema.go:1085-1087)
                 bool eq = len == nd.lit_len;
                 for (uint32_t j = 0; eq && j < len; j++)
                     eq = (dflt ? P.lits[nd.dlit + j] : arena(pay + j)) == P.lits[nd.lit + j];
@@ -921,7 +936,7 @@ __host__ __device__ uint32_t decode_blob(const DecProgram& P, const DecCols& col
 // fields are plain slices: gather them straight from the header words (all
 // read up front).  Anything else returns kFlatFallback and decode_blob runs.
 constexpr uint32_t kFlatFallback = 0xFFFFFFFFu;
-template <class R>
+template <class R, bool VAL = false>
 __device__ __forceinline__ uint32_t decode_flat(const DecProgram& P, const DecCols& cols, const R& r, uint64_t a0,
                                                 uint64_t a1, uint64_t i) {
     const int F = P.flat;
@@ -983,6 +998,7 @@ __device__ __forceinline__ uint32_t decode_flat(const DecProgram& P, const DecCo
         }
     }
     if (bad) return kFlatFallback;
+    if (VAL) return 0;   // a blob DecodeBuffer accepts, ValidateBuffer accepts
     // pass 2: the fields
     hj = h0;
     for (int j = 0; j < F; j++) {
@@ -1048,7 +1064,7 @@ __device__ __forceinline__ bool fd_null(uint32_t d) { return (d >> 23) & 1u; }
 #else
 #define DST(p, ...) __builtin_nontemporal_store((__VA_ARGS__), (p))
 #endif
-template <class R>
+template <class R, bool VAL = false>
 __device__ __forceinline__ uint32_t decode_flat_k(const FlatArg& A, const R& r, uint64_t a0, uint64_t a1, uint64_t i) {
     const int F = A.F;
     const int64_t len = (int64_t)(a1 - a0);
@@ -1073,6 +1089,7 @@ __device__ __forceinline__ uint32_t decode_flat_k(const FlatArg& A, const R& r, 
     // the End header: tag 0 and End offset == len
     bad |= (hj & 7u) != 0 || o != len;
     if (bad) return kFlatFallback;
+    if (VAL) return 0;
     o = base;
     for (int j = 0; j < F; j++) {
         const uint32_t d = A.fd[j];
@@ -1126,7 +1143,9 @@ constexpr int kDecWinChunks = 8;
 
 // WC: window chunks per blob — enough for the schema's static prefix (bytes
 // before the first var payload; compile.cpp), at most kDecWinChunks.
-template <int WC, bool EXT>
+// VAL: ValidateBuffer — status only (decode_blob<..., VAL>), P.win = the
+// bytes validation reads before the first var payload.
+template <int WC, bool EXT, bool VAL = false>
 __global__ __launch_bounds__(kBlock) PACKOS_DECWIN_ATTR void k_decode_win(DecProgram P, DecCols cols, FlatArg FA,
                                                        const uint8_t* __restrict__ arena,
                                                        const uint64_t* __restrict__ offs, uint64_t stride, uint64_t n,
@@ -1233,12 +1252,12 @@ __global__ __launch_bounds__(kBlock) PACKOS_DECWIN_ATTR void k_decode_win(DecPro
         // chunk, fits the WC chunks: a longer prefix was cut at b0 + 16 * WC)
         const bool inside = tile_mode ? (a0 >= b0 && a1 <= b0 + wbytes && a1 >= a0)
                                       : P.win > 0 && (a0 - b0) + (uint64_t)P.win <= 16ull * WC;
-        if (inside) sv = decode_flat_k(FA, LReader{(const uint32_t*)w, b0, tile_mode ? 1u : (uint32_t)kBlock}, a0, a1, i);
-        else sv = decode_flat_k(FA, R, a0, a1, i);
+        if (inside) sv = decode_flat_k<LReader, VAL>(FA, LReader{(const uint32_t*)w, b0, tile_mode ? 1u : (uint32_t)kBlock}, a0, a1, i);
+        else sv = decode_flat_k<WReader, VAL>(FA, R, a0, a1, i);
     } else if (P.flat) {
-        sv = decode_flat(LP, cols, R, a0, a1, i);
+        sv = decode_flat<WReader, VAL>(LP, cols, R, a0, a1, i);
     }
-    if (sv == kFlatFallback) sv = decode_blob<WReader, EXT>(LP, cols, R, a0, a1, i);
+    if (sv == kFlatFallback) sv = decode_blob<WReader, EXT, VAL>(LP, cols, R, a0, a1, i);
 #ifdef PACKOS_DEC_STNT
     __builtin_nontemporal_store(sv, status + i);
 #else
@@ -2321,7 +2340,9 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
     if (!status && !s->echk.empty()) {
         // EncodeValue returns ErrEncode (and no bytes) for a failing value check:
         // without a status array the failure could not be reported
-        set_error("packos_encode_batch: the schema has value checks (Range / date / prefix / suffix): status required");
+        set_error("packos_encode_batch: the schema has encode-time checks (Range / date / prefix / suffix values, or a "
+                  "named tuple whose fieldNames and schema differ / a map with an odd schema count, which fail every "
+                  "present value): status required");
         return PACKOS_E_INVALID;
     }
     int dev, r;
@@ -2691,6 +2712,58 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
         }
 #undef PACKOS_DECWIN
     }
+    HIP_TRY(hipGetLastError());
+    return PACKOS_OK;
+}
+
+// schema.ValidateBuffer (schema/schema.go:880-891) per blob: the windowed
+// SeqGetAccess decoder in its status-only VAL form, the window cut to the bytes
+// validation reads (header words, literals, checked payloads: compile.cpp).
+int packos_validate_batch(const packos_schema* cs, const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
+                          size_t n, uint32_t* status, void* stream) {
+    packos_schema* s = const_cast<packos_schema*>(cs);
+    if (!s || !status || (!arena && n)) { set_error("packos_validate_batch: bad argument"); return PACKOS_E_INVALID; }
+    if (n == 0) return PACKOS_OK;
+    if (!offsets && stride == 0) { set_error("offsets or stride required"); return PACKOS_E_INVALID; }
+    int dev, r;
+    if ((r = current_device(&dev))) return r;
+    DeviceTables* t;
+    if ((r = upload_tables(s, dev, &t))) return r;
+    int maxd = 0;
+    for (const Node& nd : s->nodes) maxd = std::max(maxd, nd.depth);
+    if (maxd >= kDecDepth) { set_error("schema nesting too deep for the decoder"); return PACKOS_E_UNSUPPORTED; }
+    DecCols dc;
+    memset(&dc, 0, sizeof(dc));
+    DecProgram P = t->dec;
+    P.win = (int32_t)s->val_win;
+    const size_t ptab = ((s->dnodes.size() * sizeof(DecNode) + 15) & ~(size_t)15) +
+                        ((s->dkids.size() * 4 + 15) & ~(size_t)15) + s->lits.size() + 16;
+    const int64_t need = s->val_win > 0 ? (s->val_win + 15 + 15) / 16 : kDecWinChunks;
+    const dim3 g((unsigned)((n + kBlock - 1) / kBlock));
+    // flat chains of plain leaves: pass 1 of the descriptor fast path only
+    FlatArg FA;
+    memset(&FA, 0, sizeof(FA));
+    {
+        const Node& root = s->nodes[0];
+        bool ok = !s->ext && !s->tune.decode_generic && !root.kids.empty() && root.kids.size() <= (size_t)kFlatMax;
+        for (size_t j = 0; ok && j < root.kids.size(); j++) {
+            const Node& nd = s->nodes[root.kids[j]];
+            const DecNode& dn = s->dnodes[root.kids[j]];
+            ok = nd.kind >= K_INT && nd.kind <= K_BYTES && nd.check == 0 && dn.width < 0x8000;
+            FA.fd[j] = (uint32_t)nd.kind | ((uint32_t)(dn.width & 0xFFFF) << 4) | ((uint32_t)dn.tag << 20) |
+                       ((dn.nullable ? 1u : 0u) << 23);
+        }
+        FA.F = ok ? (int32_t)root.kids.size() : 0;
+    }
+    hipStream_t st = (hipStream_t)stream;
+#define PACKOS_VALWIN(WC, X) \
+    hipLaunchKernelGGL((k_decode_win<WC, X, true>), g, dim3(kBlock), ptab, st, P, dc, FA, arena, offsets, stride, \
+                       (uint64_t)n, status)
+    if (s->ext) PACKOS_VALWIN(kDecWinChunks, true);
+    else if (need <= 2) PACKOS_VALWIN(2, false);
+    else if (need <= 4) PACKOS_VALWIN(4, false);
+    else PACKOS_VALWIN(kDecWinChunks, false);
+#undef PACKOS_VALWIN
     HIP_TRY(hipGetLastError());
     return PACKOS_OK;
 }

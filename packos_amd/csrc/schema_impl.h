@@ -115,6 +115,7 @@ struct packos_schema {
     int dec_fast = 0;                 // 1: canonical blob decodes (set at compile)
     int64_t dec_prefix = 0;           // bytes of an all-present blob before its first var payload
     bool dec_tail_fixed = false;      // some header / fixed / literal item follows the first var item
+    int64_t val_win = 0;              // > 0: ValidateBuffer reads nothing past this many leading bytes
 
     packos::Tune tune;
 

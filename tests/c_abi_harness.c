@@ -14,7 +14,9 @@
  *      (access/put_test.go:12-41: 17 bytes, given on the command line from
  *      tests/golden/vectors.json "put_flat17");
  *   5. packos_decode_host_batch — DecodeBuffer of every blob back into host
- *      columns; values and views must be the row's.
+ *      columns; values and views must be the row's;
+ *   6. packos_validate_host_batch — ValidateBuffer of every blob, one of
+ *      them corrupted.
  * Built by oracle/Makefile (test infrastructure), run by
  * tests/test_c_abi_harness.py on the GPU box.  Exit 0 and "c_abi_harness ok".
  *
@@ -156,6 +158,13 @@ int main(int argc, char** argv) {
         CHECK(v_len[1][i] == 2 && arena[v_start[1][i]] == 0xAA && arena[v_start[1][i] + 1] == 0xBB,
               "decoded bytes of blob %zu", i);
     }
+    /* 6. packos_validate_host_batch — ValidateBuffer of every blob (status only);
+     *    a blob whose first field header is cut to tag End fails precheck  */
+    arena[(n / 2) * (size_t)B + 2] &= 0xF8;
+    rc = packos_validate_host_batch(s, arena, offs, 0, n, dst, 0);
+    CHECK(rc == 0, "validate_host_batch: %s (%s)", packos_strerror(rc), packos_last_error());
+    for (size_t i = 0; i < n; i++)
+        CHECK(i == n / 2 ? dst[i] != 0 : dst[i] == 0, "validate status %zu = %#x", i, dst[i]);
     packos_schema_free(s);
     printf("c_abi_harness ok: %zu blobs of %d bytes\n", n, B);
     return 0;

@@ -214,8 +214,28 @@ INPUTS = [
     # derived: pack.Pack(pack.PackTuple(pack.PackInt16(7))) = 24 00 30 00 21 00 10 00 07 00
     ("pack_one_tuple_int16", "derived: pack.Pack(pack.PackTuple(pack.PackInt16(7)))", "packable",
      [TUP(I16)], [[7]]),
+    # TestValidateChain_DateEmailPrefixSuffix_Success2: pack.Pack of seven values
+    ("pack_optional_email_seven", "schema/schema_test.go:187-195 (pack.Pack of seven values)", "packable",
+     [STR, STR, I32, STR, STR, STR, STR],
+     [S(""), S("2025-09-10"), 42, S("alice@example.com"), S("prefix-hello"), S("world-suffix"), S("")]),
+    # TestSDate_SuccessAndNullable: pack.Pack(pack.PackInt64(date.Unix())) for
+    # 2025-09-10 (inside 2020..2030) and 2050-01-01 (outside), and
+    # pack.Pack(pack.PackNullableInt64(nil)) (Q2: 8 bytes of slack after End)
+    ("pack_date_2025", "schema/schema_test.go:1363-1364 (pack.Pack(PackInt64(2025-09-10)))", "packable",
+     [I64], [1757462400]),
+    ("pack_nullable_int64_nil", "schema/schema_test.go:1377 (pack.Pack(PackNullableInt64(nil)))", "packable",
+     [{"type": "int64", "nullable": True}], [None]),
+    ("pack_date_2050", "schema/schema_test.go:1386-1387 (pack.Pack(PackInt64(2050-01-01)))", "packable",
+     [I64], [2524608000]),
+    # derived: pack.Pack(pack.PackInt8(7)) = 04 00 29 00 07: a 1-byte Integer field
+    ("pack_int8_7", "derived: pack.Pack(pack.PackInt8(7))", "packable",
+     [{"type": "int8"}], [7]),
 ]
 
+SDATE_2020_2030 = {"type": "date", "nullable": True, "dateFrom": "2020-01-01T00:00:00Z",
+                   "dateTo": "2030-12-31T23:59:59Z"}     # SDate(true, from, to), schema_test.go:1356-1360
+SEVEN_SCHEMA = [STR, STR, I32R, STR, {"type": "string", "prefix": "prefix-"}, {"type": "string", "suffix": "-suffix"},
+                {"type": "string", "nullable": True, "suffix": "-suffix"}]
 PACKED_MAP = MAP(EX("meta"), MAP(EX("role"), {"type": "bytes", "width": 5}, EX("user"), {"type": "bytes", "width": 5}),
                  EX("name"), {"type": "string", "width": 6})
 PACKED_ROW = [12345, F32(3.14), 9876543210, True, {"meta": {"role": B("admin"), "user": B("alice")},
@@ -335,6 +355,77 @@ DECODE = [
     ("derived_date_width", "derived: schema/schema.go:2197-2210", "pack_date_range_email_prefix_suffix",
      [STR, {"type": "date", "dateFrom": "1970-01-01T00:01:00Z", "dateTo": "2000-01-01T00:00:00Z"}, STR, STR, STR],
      None, (3 | (2 << 8))),
+    # TestSDate_SuccessAndNullable (DecodeBuffer legs): the date decodes, the
+    # nil payload decodes as nil, 2050 fails ErrDateOutOfRange at position 0
+    ("decode_sdate_in_range", "schema/schema_test.go:1361-1375", "pack_date_2025", [SDATE_2020_2030],
+     [1757462400], 0),
+    ("decode_sdate_nil", "schema/schema_test.go:1376-1384", "pack_nullable_int64_nil", [SDATE_2020_2030],
+     [None], 0),
+    ("decode_sdate_out_of_range", "schema/schema_test.go:1385-1393", "pack_date_2050", [SDATE_2020_2030],
+     None, (14 | (1 << 8))),
+    # derived: the ValidateBuffer/DecodeBuffer divergences (VALIDATE below)
+    # SInt16(nullable) over a 1-byte Integer: DecodeBuffer panics in
+    # binary.LittleEndian.Uint16 (schema.go:649-657)
+    ("derived_short_nullable_int16", "derived: schema/schema.go:649-657", "pack_int8_7",
+     [{"type": "int16", "nullable": True}], None, (0x40000000 | (1 << 8))),
+    # SString.Optional().Suffix over "": DecodeFunc tests the empty string
+    # (schema.go:1093-1108): ErrStringSuffix at position 6
+    ("derived_optional_suffix_empty", "derived: schema/schema.go:1093-1108 over schema_test.go:187-207",
+     "pack_optional_email_seven", SEVEN_SCHEMA, None, (7 | (7 << 8))),
+    # SMap with an odd schema count: SizeExact -> ErrConstraintViolated at 4
+    # (schema.go:369-377)
+    ("derived_odd_map_decode", "derived: schema/schema.go:369-377", "schema_packed_structure",
+     [I16, F32T, I64, BOOL, MAP(EX("meta"), MAP(EX("role"), {"type": "bytes", "width": 5},
+                                               EX("user"), {"type": "bytes", "width": 5}), EX("name"))],
+     None, (3 | (5 << 8))),
+    # SString.Match("x") over "": DecodeFunc tests the empty string
+    # (schema.go:1093-1108, 1136-1142): ErrStringMatch at position 2
+    ("derived_match_empty_decode", "derived: schema/schema.go:1093-1108,1136-1142", "pack_defaults_empty",
+     [STR, I32, {"type": "string", "exact": "x"}, STR, STR], None, (9 | (3 << 8))),
+]
+
+# schema.ValidateBuffer known answers (status only; the Validate methods'
+# rules, schema.go:880-891).  Pattern / SEmail / SMapUnordered checks are
+# outside the compiled subset: as in DECODE, they are dropped (a plain string)
+VALIDATE = [
+    ("validate_packed_structure", "schema/schema_test.go:15-50", "schema_packed_structure",
+     [I16R, F32T, I64, BOOL, PACKED_MAP], 0),
+    # wrong width for "admin": SBytes(6): the inner SMap's precheck fails,
+    # wrapped by both maps as ErrInvalidFormat at top-level position 4
+    ("validate_packed_structure_failure", "schema/schema_test.go:52-89", "schema_packed_structure",
+     [I16, F32T, I64, BOOL, MAP(EX("meta"), MAP(EX("role"), {"type": "bytes", "width": 6},
+                                               EX("user"), {"type": "bytes", "width": 5}),
+                               EX("name"), {"type": "string", "width": 6})], (1 | (5 << 8))),
+    ("validate_prefix_suffix", "schema/schema_test.go:166-185 (Pattern checks dropped)",
+     "pack_date_range_email_prefix_suffix",
+     [STR, I32R, STR, {"type": "string", "prefix": "prefix-"}, {"type": "string", "suffix": "-suffix"}], 0),
+    # SString.Optional().Suffix("-suffix") over "" passes Validate
+    # (schema.go:1085-1087); SEmail / Pattern dropped
+    ("validate_optional_suffix_empty", "schema/schema_test.go:187-211 (SEmail / Pattern dropped)",
+     "pack_optional_email_seven", SEVEN_SCHEMA, 0),
+    ("validate_packed_tuples", "schema/schema_test.go:213-242", "pack_two_tuples34",
+     [TUP(I32, BOOL, {"type": "string", "width": 2}), TUP(I16, BOOL, {"type": "string", "width": 2})], 0),
+    ("validate_sdate_in_range", "schema/schema_test.go:1361-1368", "pack_date_2025", [SDATE_2020_2030], 0),
+    ("validate_sdate_nil", "schema/schema_test.go:1376-1379", "pack_nullable_int64_nil", [SDATE_2020_2030], 0),
+    ("validate_sdate_out_of_range", "schema/schema_test.go:1385-1389", "pack_date_2050", [SDATE_2020_2030],
+     (14 | (1 << 8))),
+    # derived: SInt16(nullable).Validate = validatePrimitive, which never reads
+    # the payload (schema.go:646-648): a 1-byte Integer passes
+    ("derived_validate_short_nullable_int16", "derived: schema/schema.go:646-648", "pack_int8_7",
+     [{"type": "int16", "nullable": True}], 0),
+    # derived: SDateRange's ValidateFunc reads the payload like its DecodeFunc
+    # (schema.go:2198-2212): a 4-byte payload under a nullable date panics in both
+    ("derived_validate_short_date_panics", "derived: schema/schema.go:2198-2212",
+     "pack_date_range_email_prefix_suffix", [STR, {"type": "date", "nullable": True}, STR, STR, STR],
+     (0x40000000 | (2 << 8))),
+    # derived: SchemaMap.Validate has no odd-count check (schema.go:336-359):
+    # the three schemas validate in sequence over the four fields
+    ("derived_validate_odd_map", "derived: schema/schema.go:336-359", "schema_packed_structure",
+     [I16, F32T, I64, BOOL, MAP(EX("meta"), MAP(EX("role"), {"type": "bytes", "width": 5},
+                                               EX("user"), {"type": "bytes", "width": 5}), EX("name"))], 0),
+    # derived: Match over "" passes ValidateFunc (nullable receiver SString)
+    ("derived_validate_match_empty", "derived: schema/schema.go:1072-1091,1136-1142",
+     "pack_defaults_empty", [STR, I32, {"type": "string", "exact": "x"}, STR, STR], 0),
 ]
 
 
@@ -366,10 +457,15 @@ def main():
     for cid, src, from_case, schema, row, status in DECODE:
         out["decode"].append({"id": cid, "source": src, "input_from": from_case, "schema": schema,
                               "expect_row": row, "expect_status": status})
+    out["validate"] = []
+    for cid, src, from_case, schema, status in VALIDATE:
+        out["validate"].append({"id": cid, "source": src, "input_from": from_case, "schema": schema,
+                                "expect_status": status})
     with open(OUT, "w") as f:
         json.dump(out, f, indent=1)
     print(f"wrote {OUT}: {len(out['encode'])} encode, {len(out['equal'])} equal, "
-          f"{len(out['get'])} get, {len(out['maps'])} maps, {len(out['seq'])} seq, {len(out['inputs'])} inputs, {len(out['decode'])} decode")
+          f"{len(out['get'])} get, {len(out['maps'])} maps, {len(out['seq'])} seq, {len(out['inputs'])} inputs, {len(out['decode'])} decode, "
+          f"{len(out['validate'])} validate")
 
 
 if __name__ == "__main__":

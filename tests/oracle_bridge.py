@@ -68,6 +68,8 @@ def lib():
                                       C.c_size_t, C.POINTER(PackosColumn), C.c_void_p, C.c_int]
         L.or_decode_batch_mode.argtypes = [C.POINTER(OrSchema), C.c_void_p, C.c_void_p, C.c_uint64,
                                            C.c_size_t, C.POINTER(PackosColumn), C.c_void_p, C.c_int, C.c_int]
+        L.or_validate_batch.argtypes = [C.POINTER(OrSchema), C.c_void_p, C.c_void_p, C.c_uint64,
+                                        C.c_size_t, C.c_void_p, C.c_int, C.c_int]
         L.or_seq_init_ext.argtypes = [C.POINTER(OrSeq), C.c_void_p, C.c_int64, C.c_int]
         L.or_get_init.argtypes = [C.POINTER(OrGet), C.c_void_p, C.c_int64]
         L.or_get_fixed.argtypes = [C.POINTER(OrGet), C.c_int64, C.c_int, C.c_int,
@@ -237,6 +239,19 @@ def decode(chain, arena: np.ndarray, offsets: Optional[np.ndarray], n: int, stri
     lib().or_decode_batch_mode(C.byref(os_.s), _ptr(a), _ptr(o), stride, n, out.cols(), _ptr(st),
                                nthreads, mode)
     return out, st[:n]
+
+
+def validate(chain, arena: np.ndarray, offsets: Optional[np.ndarray], n: int, stride: int = 0,
+             nthreads=1, mode=0):
+    """or_validate_batch: ValidateBuffer's status word per blob."""
+    os_ = OracleSchema(chain)
+    st = np.zeros(max(n, 1), np.uint32)
+    a = np.ascontiguousarray(arena, dtype=np.uint8)
+    if a.size == 0:
+        a = np.zeros(1, np.uint8)
+    o = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+    lib().or_validate_batch(C.byref(os_.s), _ptr(a), _ptr(o), stride, n, _ptr(st), nthreads, mode)
+    return st[:n]
 
 
 def get_field_batch(arena, offsets, n, path, want_tag, want_width, stride=0):

@@ -28,7 +28,7 @@ def test_exports_match_header():
     for name in sorted(declared):
         assert hasattr(L, name), f"{name} declared in packos.h but not exported"
     assert set(_lib.EXPORTED) == declared
-    assert L.packos_abi_version() == 3
+    assert L.packos_abi_version() == 4
 
 
 def test_schema_errors():
@@ -36,8 +36,15 @@ def test_schema_errors():
     h = C.c_void_p()
     assert L.packos_schema_compile(b"[{\"type\":\"email\"}]", 0, C.byref(h)) == -3
     assert b"outside" in L.packos_last_error()
+    # map keys must be strings (the compiled subset)
+    assert L.packos_schema_compile(b"[{\"type\":\"map\",\"schema\":[{\"type\":\"int16\"},{\"type\":\"int16\"}]}]",
+                                   0, C.byref(h)) == -2
+    # an odd SMap schema count compiles (Validate accepts it, schema.go:336-359);
+    # encode of a present value fails, so the schema needs a status array
     assert L.packos_schema_compile(b"[{\"type\":\"map\",\"schema\":[{\"type\":\"string\"}]}]", 0,
-                                   C.byref(h)) == -2
+                                   C.byref(h)) == 0
+    assert L.packos_schema_has_checks(h) == 1
+    L.packos_schema_free(h)
     assert L.packos_schema_compile(b"[{\"type\":", 0, C.byref(h)) == -2
     assert L.packos_schema_compile(b"[{\"type\":\"string\",\"pattern\":\"^a\"}]", 0, C.byref(h)) == -3
     assert L.packos_schema_compile(b"[{\"type\":\"int16\",\"min\":0.5}]", 0, C.byref(h)) == -2

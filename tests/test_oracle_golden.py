@@ -4,6 +4,8 @@ Every byte vector comes from the reference test sources via
 tests/golden/make_golden.py; a failure here means the oracle is not a faithful
 restatement and no GPU parity claim can rest on it.
 """
+import json
+
 import numpy as np
 import pytest
 
@@ -254,3 +256,31 @@ def test_decode_golden(case):
             o = exp.offsets[c]
             got = sp.node.default[:ln] if s0 == VIEW_DEFAULT else blob[s0:s0 + ln]
             assert got == bytes(exp.data[c][o[0]:o[1]]), (case["id"], c)
+
+
+@pytest.mark.parametrize("case", G["validate"], ids=[c["id"] for c in G["validate"]])
+def test_validate_golden(case):
+    """ValidateBuffer known answers (schema_test.go) and the derived cases
+    where Validate's rules differ from DecodeBuffer's."""
+    blob = _golden_bytes(case["input_from"])
+    chain = chain_of(case["schema"])
+    st = ob.validate(chain, np.frombuffer(blob, np.uint8), np.asarray([0, len(blob)], np.uint64), 1)
+    assert int(st[0]) == case["expect_status"], hex(int(st[0]))
+
+
+def test_validate_vs_decode_divergences():
+    """Each derived Validate case whose schema also appears in DECODE gives the
+    two different answers the reference's two code paths give."""
+    dec = {(c["input_from"], json.dumps(c["schema"], sort_keys=True)): c["expect_status"] for c in G["decode"]}
+    pairs = 0
+    for c in G["validate"]:
+        k = (c["input_from"], json.dumps(c["schema"], sort_keys=True))
+        if k in dec:
+            pairs += 1
+            blob = _golden_bytes(c["input_from"])
+            chain = chain_of(c["schema"])
+            a = np.frombuffer(blob, np.uint8)
+            o = np.asarray([0, len(blob)], np.uint64)
+            assert int(ob.validate(chain, a, o, 1)[0]) == c["expect_status"]
+            assert int(ob.decode(chain, a, o, 1)[1][0]) == dec[k]
+    assert pairs >= 6
