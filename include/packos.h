@@ -289,6 +289,14 @@ int packos_encoded_size_batch(const packos_schema* s, const packos_column* cols,
  * kernel even when the lane-invariant one applies; variable-size batches use
  * the generic one-wavefront-per-blob kernel instead of the tiled one         */
 #define PACKOS_ENC_FORCE_GENERIC 2u
+/* out_capacity is the batch's exact encoded size (e.g. out_offsets[n] of
+ * packos_encoded_size_batch): the library takes out_capacity / n as the mean
+ * blob size when it picks the kernel for a flat chain of leaves with every
+ * value present.  Without it, a batch whose capacity admits >= 256 bytes per
+ * blob has its var columns' first and last offsets read back (a small copy
+ * on `stream` and a wait for it) to compute that mean.  Results never depend
+ * on the choice.                                                             */
+#define PACKOS_ENC_CAP_EXACT 4u
 /* testing/benchmark knob: pick the fixed-layout kernel variant (0 = auto):
  * 13 one tile per workgroup, LDS-DMA staging, single-source dwords (auto
  *    when B % 4 == 0, 16 <= B <= 1024, <= 16 fixed columns);
@@ -497,7 +505,7 @@ const char* packos_last_error(void);   /* thread-local detail of the last failur
 int         packos_abi_version(void);
 /* Diagnostics: the encode kernel the last packos_encode_batch call of this
  * thread launched ("fixed_tile", "fixed_dw", "fixed", "var", "ext", "flat",
- * "tiles", "" before any call).  No reference counterpart; tests use it to
+ * "tiles"; "" before any call and after a call that launched none).  No reference counterpart; tests use it to
  * assert which encoder a batch exercised.                                      */
 const char* packos_last_encoder(void);
 

@@ -18,6 +18,7 @@ MODE_PACKABLE = 1
 MODE_EXTENDED = 0x100   # ADR-001 extended containers (include/packos.h), OR-ed into a mode
 ENC_OFFSETS_READY = 1
 ENC_FORCE_GENERIC = 2
+ENC_CAP_EXACT = 4       # out_capacity is the batch's exact encoded size (kernel choice without a read-back)
 
 
 def ENC_FIXED_VARIANT(v: int) -> int:

@@ -223,9 +223,13 @@ def encode_batch(schema: CompiledSchema, cols: DeviceColumns, want_offsets: bool
     total = int(offs[n].item()) if n else 0
     if out is None or out.numel() < total:
         out = torch.empty(max(total, 16), dtype=torch.uint8, device=dev)
+    if cols.any_valid():
+        flags |= _lib.ENC_OFFSETS_READY   # presence depends on the data: keep the size pass's layout
+    elif out.numel() == total:
+        flags |= _lib.ENC_CAP_EXACT       # closed form: the encoder writes the same offsets itself
     check(L.packos_encode_batch(schema.handle, arr, n, out.data_ptr(), out.numel(), offs.data_ptr(),
                                 None if status is None else status.data_ptr(), ws.data_ptr(), wsb,
-                                _lib.ENC_OFFSETS_READY | flags, st), "packos_encode_batch")
+                                flags, st), "packos_encode_batch")
     return EncodeResult(out, offs, status[:n] if status is not None else None, total, -1)
 
 
@@ -421,6 +425,8 @@ class EncodePlan:
         self.out = out if out is not None else torch.empty(max(self.total, 16), dtype=torch.uint8, device=dev)
         if self.out.numel() < self.total:
             raise ValueError("EncodePlan: `out` is smaller than the batch's encoded size")
+        if not self.fixed and self.out.numel() == self.total:
+            self.flags |= _lib.ENC_CAP_EXACT   # the arena is the batch's exact size (from the size pass)
 
     def run(self):
         L = lib()

@@ -856,12 +856,8 @@ void read_tune(Tune& t) {
     t.sizes_scan = getenv("PACKOS_SIZES_SCAN") != nullptr;
     t.decode_generic = getenv("PACKOS_DECODE_GENERIC") != nullptr;
     if (const char* e = getenv("PACKOS_DEC_TILE_BYTES")) t.dec_tile_bytes = std::min(49152, std::max(1024, atoi(e)));
-    if (const char* e = getenv("PACKOS_DEC_PERSIST")) t.dec_persist = std::min(2, std::max(0, atoi(e)));
-    if (const char* e = getenv("PACKOS_DEC_PERSIST_GRID")) t.dec_persist_grid = std::max(0, atoi(e));
     if (const char* e = getenv("PACKOS_ENC_FLAT")) t.enc_flat = atoi(e);
     if (const char* e = getenv("PACKOS_DEC_W16")) t.dec_w16 = atoi(e) != 0;
-    if (const char* e = getenv("PACKOS_FLAT_GL")) t.flat_gl = atoi(e) == 8 || atoi(e) == 16 || atoi(e) == 64 ? atoi(e) : 0;
-    if (const char* e = getenv("PACKOS_FLAT_W")) t.flat_w = std::max(0, std::min(24576, atoi(e) & ~15));
 }
 
 // Same rule as the device's ext_layout_wave (kernels.hip): containers in

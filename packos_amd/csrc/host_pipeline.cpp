@@ -320,11 +320,12 @@ int packos_pipeline::encode_impl(const packos_column* hc, size_t n, uint8_t* hos
         // kernels: after the inputs, and after chunk k - S's outputs left the slot
         HP_TRY(hipStreamWaitEvent(comp, sl.ev_in, 0));
         if (k >= S) HP_TRY(hipStreamWaitEvent(comp, sl.ev_out, 0));
-        // closed form: the chunk's exact size (the var encoder is picked by the
-        // bytes per blob, so it must not see the grow-only buffer's headroom)
+        // closed form: the chunk's exact size, so the var encoder is picked by
+        // the bytes per blob without reading the offsets back
         HP_RC(packos_encode_batch(s, dc.data(), m, sl.eout.as<uint8_t>(), closed ? total[k] : sl.eout.cap,
                                   fixed_size ? nullptr : sl.eoffs.as<uint64_t>(),
-                                  host_status ? sl.estatus.as<uint32_t>() : nullptr, sl.ews.p, sl.ews.cap, 0, comp));
+                                  host_status ? sl.estatus.as<uint32_t>() : nullptr, sl.ews.p, sl.ews.cap,
+                                  closed ? PACKOS_ENC_CAP_EXACT : 0u, comp));
         if (!closed)
             HP_TRY(hipMemcpyAsync(sl.htotal.p, sl.eoffs.as<uint64_t>() + m, sizeof(uint64_t), hipMemcpyDeviceToHost, comp));
         HP_TRY(hipEventRecord(sl.ev_comp, comp));

@@ -1290,11 +1290,28 @@ struct DecColsK {
 
 __device__ __forceinline__ uint32_t lds_u8(const uint32_t* lds, uint32_t a) { return (lds[a >> 2] >> (8 * (a & 3))) & 0xFFu; }
 
+// 16 bytes at LDS byte q; m = q & 15 wave-uniform: two ds_read_b128 and a
+// byte shift chosen by a scalar branch
+__device__ __forceinline__ u32x4 lds16u(const uint8_t* lds, uint32_t q, uint32_t m) {
+    const uint32_t qa = q - m;
+    const u32x4 x0 = *(const u32x4*)(lds + qa);
+    if (m == 0) return x0;
+    const u32x4 x1 = *(const u32x4*)(lds + qa + 16);
+    const uint32_t sh = m & 3u;
+#define AB(h, l) __builtin_amdgcn_alignbyte(h, l, sh)
+    switch (m >> 2) {
+        case 0: return u32x4{AB(x0.y, x0.x), AB(x0.z, x0.y), AB(x0.w, x0.z), AB(x1.x, x0.w)};
+        case 1: return u32x4{AB(x0.z, x0.y), AB(x0.w, x0.z), AB(x1.x, x0.w), AB(x1.y, x1.x)};
+        case 2: return u32x4{AB(x0.w, x0.z), AB(x1.x, x0.w), AB(x1.y, x1.x), AB(x1.z, x1.y)};
+        default: return u32x4{AB(x1.x, x0.w), AB(x1.y, x1.x), AB(x1.z, x1.y), AB(x1.w, x1.z)};
+    }
+#undef AB
+}
+
 // Steps 2-4 of a staged tile (constant-byte and value checks -> fail flags,
 // column stores, validity) by NCT threads, this one being thread ct; the
 // tile's rows start at lds_raw.  Then, after a barrier, dfix_status: every
-// row's status, failed rows through decode_blob (clear: reset the row's fail
-// flag for the next tile of a persistent workgroup).
+// row's status, failed rows through decode_blob.
 template <int NCT>
 __device__ __forceinline__ void dfix_tile(const DecFixProgram& F, const DecProgram& P, const DecCols& cols,
                                           const DecColsK& K, const uint8_t* lds_raw, const uint32_t* chk,
@@ -1411,13 +1428,11 @@ __device__ __forceinline__ void dfix_tile(const DecFixProgram& F, const DecProgr
 template <bool EXT, int NCT>
 __device__ __forceinline__ void dfix_status(const DecProgram& P, const DecCols& cols, const uint8_t* arena,
                                             const uint64_t* offs, uint32_t B, uint32_t* status, uint32_t* fail,
-                                            uint64_t blob0, uint32_t rows, uint32_t ct, bool clear) {
+                                            uint64_t blob0, uint32_t rows, uint32_t ct) {
     for (uint32_t j = ct; j < rows; j += NCT) {
         const uint64_t i = blob0 + j;
         uint32_t sv = 0;
-        const bool f = fail[j] != 0;
-        if (clear) fail[j] = 0;
-        if (f)
+        if (fail[j] != 0)
             sv = decode_blob<GReader, EXT>(P, cols, GReader{arena}, offs ? offs[i] : i * B,
                                            offs ? offs[i + 1] : (i + 1) * B, i);
 #ifdef PACKOS_DEC_STNT
@@ -1501,7 +1516,7 @@ __device__ __forceinline__ void dfix_oneshot(const DecFixProgram& F, const DecPr
     }
     dfix_tile<kBlock>(F, P, cols, K, lds_raw, chk, fail, blob0, rows, (uint32_t)tid);
     __syncthreads();
-    dfix_status<EXT, kBlock>(P, cols, arena, offs, B, status, fail, blob0, rows, (uint32_t)tid, false);
+    dfix_status<EXT, kBlock>(P, cols, arena, offs, B, status, fail, blob0, rows, (uint32_t)tid);
 }
 
 template <bool EXT>
@@ -1520,104 +1535,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     DecFixProgram F, DecProgram P, DecCols cols, DecColsK K, const uint8_t* __restrict__ arena,
     const uint64_t* __restrict__ offs, uint64_t n, uint32_t* __restrict__ status, uint64_t tile0) {
     dfix_oneshot<EXT>(F, P, cols, K, arena, offs, n, status, tile0);
-}
-
-// Persistent form (full tiles only; opt-in, PACKOS_DEC_PERSIST): one
-// workgroup walks tiles blockIdx.x, + gridDim.x, ... with two LDS tile
-// buffers.  Wave 0 is the producer: it issues tile k + 1's staging DMA (and
-// the DMA of its offsets) while waves 1..7 write tile k's columns, so the HBM
-// round trip of a tile's rows no longer sits in front of every tile's
-// stores.  The producer issues nothing but DMA, so its vmcnt(0) waits for
-// exactly the tile it needs; the consumer waves never wait on their stores.
-// Measured slower (round 4, same box): M decode 0.098 -> 0.157 ms, C2 0.0315
-// -> 0.052, C4 0.42 -> 0.59.  A tile's column phase, not its load, is the
-// long pole (~11 us per tile either way), and three 8-wave workgroups per CU
-// write half as many tiles at once as six one-shot workgroups.
-constexpr int kDecPBlock = 512, kDecPCons = kDecPBlock - kWave;
-#ifndef PACKOS_DECFIXP_ATTR
-// <= 80 VGPRs: three 8-wave workgroups per CU (the 2 x 24-KB buffers admit three)
-#define PACKOS_DECFIXP_ATTR __attribute__((amdgpu_waves_per_eu(6, 8)))
-#endif
-template <bool EXT>
-__global__ __launch_bounds__(kDecPBlock) PACKOS_DECFIXP_ATTR void k_decode_fixed_p(
-    DecFixProgram F, DecProgram P, DecCols cols, DecColsK K, const uint8_t* __restrict__ arena,
-    const uint64_t* __restrict__ offs, uint64_t ntiles, uint32_t* __restrict__ status) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds_raw[];
-    const uint32_t B = (uint32_t)F.B, T = (uint32_t)F.T, QW = (B + 3) >> 2;
-    const uint32_t TB = T * B;                              // a multiple of 16 (T % 16 == 0)
-    uint64_t* ob = (uint64_t*)(lds_raw + 2 * TB);           // buffer b's offsets at ob + b T
-    uint32_t* chk = (uint32_t*)(ob + 2 * T);
-    uint32_t* fail = chk + 3 * QW;
-    uint32_t* okf = fail + T;                               // okf[b]: buffer b's tile is contiguous
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const bool producer = tid < (uint32_t)kWave;
-    const uint64_t G = gridDim.x;
-    typedef __attribute__((address_space(4))) const uint64_t c_u64;
-    const uint32_t lds0 = (uint32_t)(uintptr_t)lds_raw;
-    // producer: stage tile tt into buffer bb; returns its base offset and
-    // whether its range is the expected aligned T * B bytes (else nothing is
-    // staged and the tile takes the per-blob path)
-    auto issue = [&](uint64_t tt, uint32_t bb, uint64_t& base) -> bool {
-        const uint64_t blob0 = tt * T;
-        base = blob0 * B;
-        uint64_t end = base + TB;
-        if (offs) {
-            base = ((c_u64*)(uintptr_t)offs)[blob0];
-            end = ((c_u64*)(uintptr_t)offs)[blob0 + T];
-        }
-        const bool okp = (base & 15) == 0 && end >= base && end - base == TB;
-        if (okp) {
-            const uint8_t* src = arena + base;
-            const uint32_t lb = lds0 + bb * TB;
-            for (uint32_t c0 = 0; c0 < TB / 16; c0 += kWave)
-                if (c0 + lane < TB / 16) dma16nt(src + 16u * (c0 + lane), __builtin_amdgcn_readfirstlane(lb + 16u * c0));
-            if (offs) {   // offs[blob0 .. blob0 + T) (16-B aligned: host check, T % 16 == 0)
-                const uint8_t* os = (const uint8_t*)(offs + blob0);
-                const uint32_t lo = (uint32_t)(uintptr_t)(ob + bb * T);
-                for (uint32_t c0 = 0; c0 < T / 2; c0 += kWave)
-                    if (c0 + lane < T / 2) dma16(os + 16u * (c0 + lane), __builtin_amdgcn_readfirstlane(lo + 16u * c0));
-            }
-        }
-        return okp;
-    };
-    uint64_t t = blockIdx.x, cur_base = 0;
-    bool cur_okp = false;
-    if (producer && t < ntiles) cur_okp = issue(t, 0, cur_base);
-    // the check table (its load queues behind the first tile's DMA)
-    const uint32_t nchk = 3u * (uint32_t)F.n_chk;
-    for (uint32_t q = tid; q < nchk; q += kDecPBlock) chk[q] = F.chk[q];
-    for (uint32_t j = tid; j < T; j += kDecPBlock) fail[j] = 0;
-    for (uint32_t k = 0; t < ntiles; k++, t += G) {
-        const uint32_t b = k & 1;
-        if (producer) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t's rows and offsets
-            bool ok = cur_okp;
-            if (ok && offs)
-                for (uint32_t j = lane; j < T; j += kWave) ok &= ob[b * T + j] == cur_base + (uint64_t)j * B;
-            ok = __builtin_amdgcn_ballot_w64(!ok) == 0;   // wave-wide AND (every lane active)
-            if (lane == 0) okf[b] = ok ? 1u : 0u;
-        }
-        __syncthreads();   // buffer b staged, okf[b] set; buffer b ^ 1 free
-        const bool ok = okf[b] != 0;
-        const uint64_t blob0 = t * T;
-        if (producer) {
-            if (t + G < ntiles) cur_okp = issue(t + G, b ^ 1, cur_base);
-        } else if (ok) {
-            dfix_tile<kDecPCons>(F, P, cols, K, lds_raw + b * TB, chk, fail, blob0, T, tid - kWave);
-        }
-        __syncthreads();   // fail flags of tile t set; buffer b read
-        if (!producer) {
-            if (ok) {
-                dfix_status<EXT, kDecPCons>(P, cols, arena, offs, B, status, fail, blob0, T, tid - kWave, true);
-            } else {
-                for (uint32_t j = tid - kWave; j < T; j += kDecPCons) {
-                    const uint64_t i = blob0 + j;
-                    status[i] = decode_blob<GReader, EXT>(P, cols, GReader{arena}, offs ? offs[i] : i * B,
-                                                          offs ? offs[i + 1] : (i + 1) * B, i);
-                }
-            }
-        }
-    }
 }
 
 // =========================================================================
@@ -2005,35 +1922,6 @@ int current_device(int* dev) {
     return PACKOS_OK;
 }
 
-// compute units of device dev (cached; 256 on MI355X)
-int num_cus(int dev) {
-    static std::mutex mu;
-    static std::map<int, int> cache;
-    std::lock_guard<std::mutex> g(mu);
-    auto it = cache.find(dev);
-    if (it != cache.end()) return it->second;
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 1;
-    cache[dev] = cus;
-    return cus;
-}
-
-// resident workgroups per CU of a kernel at (block, dynamic LDS) (cached)
-template <typename K>
-int occupancy(K kern, int block, size_t lds) {
-    static std::mutex mu;
-    static std::map<std::pair<const void*, size_t>, int> cache;
-    std::lock_guard<std::mutex> g(mu);
-    const auto key = std::make_pair((const void*)kern, lds);
-    auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, block, lds) != hipSuccess || nb <= 0) nb = 1;
-    cache[key] = nb;
-    return nb;
-}
-
-
 // Does the all-present blob of a fixed schema decode cleanly?  Runs the same
 // decode_blob the device runs, on the host, over the canonical blob (zero
 // payload bytes).  Only then may k_decode_fixed treat "constant bytes match"
@@ -2324,6 +2212,33 @@ int packos_encoded_size_batch(const packos_schema* cs, const packos_column* cols
     return size_pass(s, t, ec, n, out_offsets, ws, ws_bytes, st);
 }
 
+static thread_local const char* g_last_encoder = "";   // packos_last_encoder
+
+// Mean encoded blob size of a closed-form batch: n * C static bytes plus the
+// var columns' byte ranges (off[n] - off[0]).  PACKOS_ENC_CAP_EXACT: the
+// caller's out_capacity is the batch's exact size; otherwise the 2 offsets per
+// var column are read back (a 16-B-per-column copy on the call's stream and a
+// wait for it: only for batches whose capacity admits >= kFlatMinBlob per blob).
+static int mean_blob_bytes(const AffPlan& A, size_t n, uint64_t cap, uint32_t flags, hipStream_t st, uint64_t* mean) {
+    if ((flags & PACKOS_ENC_CAP_EXACT) || A.nv == 0) {
+        *mean = (A.nv == 0 ? A.C * n : cap) / n;
+        return PACKOS_OK;
+    }
+    static thread_local uint64_t* pin = nullptr;   // 2 words per var column, pinned once per thread
+    if (!pin) HIP_TRY(hipHostMalloc((void**)&pin, 2 * kAffVar * sizeof(uint64_t), hipHostMallocDefault));
+    for (int v = 0; v < A.nv; v++) {
+        const size_t w = ((A.w8 >> v) & 1u) ? 8 : 4;
+        pin[2 * v] = pin[2 * v + 1] = 0;
+        HIP_TRY(hipMemcpyAsync(&pin[2 * v], A.off[v], w, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&pin[2 * v + 1], (const uint8_t*)A.off[v] + n * w, w, hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    uint64_t bytes = A.C * n;
+    for (int v = 0; v < A.nv; v++) bytes += pin[2 * v + 1] - pin[2 * v];
+    *mean = bytes / n;
+    return PACKOS_OK;
+}
+
 static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& ec, bool any_nil, size_t n,
                              uint8_t* out, uint64_t cap, uint64_t* out_offsets, uint32_t* status, void* ws,
                              size_t ws_bytes, uint32_t flags, hipStream_t st);
@@ -2332,6 +2247,7 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
                         uint64_t* out_offsets, uint32_t* status, void* ws, size_t ws_bytes, uint32_t flags,
                         void* stream) {
     packos_schema* s = const_cast<packos_schema*>(cs);
+    g_last_encoder = "";
     if (!s || !cols || (!out && n)) { set_error("packos_encode_batch: bad argument"); return PACKOS_E_INVALID; }
     if (n == 0) {
         if (out_offsets) HIP_TRY(hipMemsetAsync(out_offsets, 0, sizeof(uint64_t), (hipStream_t)stream));
@@ -2365,8 +2281,6 @@ int packos_encode_batch(const packos_schema* cs, const packos_column* cols, size
     return PACKOS_OK;
 }
 
-static thread_local const char* g_last_encoder = "";
-const char* packos_last_encoder(void) { return g_last_encoder; }
 
 static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& ec, bool any_nil, size_t n,
                              uint8_t* out, uint64_t cap, uint64_t* out_offsets, uint32_t* status, void* ws,
@@ -2473,40 +2387,26 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
     // flat closed-form chains of large blobs: k_encode_flat (encode_flat.inc).
     // Small blobs stay on k_encode_tiles, whose frame builds the whole output
     // image in LDS (C3, 85-B blobs: 0.060 ms there vs 0.106 ms here); large
-    // blobs stream their values straight from HBM here (C5, 969-B blobs: 3.97
-    // ms vs 4.29).  The blob sizes are device data: `cap` (the arena the caller
-    // sized, normally from packos_encoded_size_batch) stands in for them.
-    const bool flat_ok = s->tune.enc_flat == 1 || (s->tune.enc_flat == 2 && n && cap / n >= kFlatMinBlob);
-    if (flat_ok && !offs_ready && !(flags & PACKOS_ENC_FORCE_GENERIC) && affine_layout(s, ec, nullptr)) {
+    // blobs stream their values straight from HBM here (C5, 969-B blobs: 3.57
+    // ms vs 4.29).  The choice follows the batch's mean blob size: the static
+    // bytes plus the var bytes (mean_blob_bytes).
+    AffPlan A;
+    if (s->tune.enc_flat != 0 && !offs_ready && !(flags & PACKOS_ENC_FORCE_GENERIC) && affine_layout(s, ec, &A)) {
+        bool flat_ok = s->tune.enc_flat == 1;
+        if (!flat_ok && n && cap / n >= kFlatMinBlob) {   // cap / n bounds the mean from above
+            uint64_t mean = 0;
+            if ((r = mean_blob_bytes(A, n, cap, flags, st, &mean))) return r;
+            flat_ok = mean >= kFlatMinBlob;
+        }
         FPlan F;
-        if (flat_plan(s, ec, F, (uint32_t)s->tune.flat_w)) {
+        if (flat_ok && flat_plan(s, ec, F)) {
             const dim3 g((unsigned)((n + kFT - 1) / kFT));
-            g_last_encoder = F.wbytes ? "flat_s" : "flat";
-#define PACKOS_FLAT(K, NV) \
-    hipLaunchKernelGGL((K<NV>), g, dim3(kFNT), F.lds_total, st, F, out_offsets, out, cap, (uint64_t)n, status)
-            if (F.wbytes) {
-                // lanes per blob by the mean blob (the arena per blob): 8 up to
-                // 112 B (<= 7 chunks + the shared edge), 16 up to 240 B, else a wave
-                const uint64_t mb = n ? cap / n : 0;
-                const int gl = s->tune.flat_gl ? s->tune.flat_gl : mb <= 112 ? 8 : mb <= 240 ? 16 : 64;
-#define PACKOS_FLATS(NV)                                                                  \
-    do {                                                                                  \
-        if (gl == 8) hipLaunchKernelGGL((k_encode_flat_s<NV, 8>), g, dim3(kFNT), F.lds_total, st, F, \
-                                        out_offsets, out, cap, (uint64_t)n, status);      \
-        else if (gl == 16) hipLaunchKernelGGL((k_encode_flat_s<NV, 16>), g, dim3(kFNT), F.lds_total, st, F, \
-                                              out_offsets, out, cap, (uint64_t)n, status); \
-        else hipLaunchKernelGGL((k_encode_flat_s<NV, 64>), g, dim3(kFNT), F.lds_total, st, F, \
-                                out_offsets, out, cap, (uint64_t)n, status);              \
-    } while (0)
-                if (F.nvar <= 1) PACKOS_FLATS(1);
-                else if (F.nvar <= 2) PACKOS_FLATS(2);
-                else PACKOS_FLATS(4);
-#undef PACKOS_FLATS
-            } else {
-                if (F.nvar <= 1) PACKOS_FLAT(k_encode_flat, 1);
-                else if (F.nvar <= 2) PACKOS_FLAT(k_encode_flat, 2);
-                else PACKOS_FLAT(k_encode_flat, 4);
-            }
+            g_last_encoder = "flat";
+#define PACKOS_FLAT(NV) \
+    hipLaunchKernelGGL((k_encode_flat<NV>), g, dim3(kFNT), F.lds_total, st, F, out_offsets, out, cap, (uint64_t)n, status)
+            if (F.nvar <= 1) PACKOS_FLAT(1);
+            else if (F.nvar <= 2) PACKOS_FLAT(2);
+            else PACKOS_FLAT(4);
 #undef PACKOS_FLAT
             HIP_TRY(hipGetLastError());
             return PACKOS_OK;
@@ -2583,6 +2483,8 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
     return PACKOS_OK;
 }
 
+const char* packos_last_encoder(void) { return g_last_encoder; }
+
 int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
                         size_t n, packos_column* out_cols, uint32_t* status, void* stream) {
     packos_schema* s = const_cast<packos_schema*>(cs);
@@ -2640,22 +2542,7 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
             K.flags[c] = f.flags | (s->tune.dec_w16 ? 0u : 2u);
             K.magic[c] = f.magic;
         }
-        // persistent double-buffered workgroups over the full tiles (offsets
-        // staged by DMA: 16-B aligned), the last partial tile one-shot
-        uint64_t full = n / T, tile0 = 0;
-        const bool persist = ((uintptr_t)offsets & 15) == 0 && full > 0 &&
-                             (s->tune.dec_persist == 2 || (s->tune.dec_persist == 1 && full >= 2 * (uint64_t)num_cus(dev)));
-        if (persist) {
-            const size_t lp = 2 * (size_t)T * B + 16 * (size_t)T + 12 * QW + 4 * (size_t)T + 16;
-            auto kp = s->ext ? k_decode_fixed_p<true> : k_decode_fixed_p<false>;
-            uint64_t slots = (uint64_t)num_cus(dev) * (uint64_t)occupancy(kp, kDecPBlock, lp);
-            if (s->tune.dec_persist_grid > 0) slots = std::min<uint64_t>(slots, (uint64_t)s->tune.dec_persist_grid);
-            const uint64_t per = (full + slots - 1) / slots;   // tiles per workgroup
-            const uint64_t G = (full + per - 1) / per;
-            hipLaunchKernelGGL(kp, dim3((unsigned)G), dim3(kDecPBlock), lp, st, F, t->dec, dc, K, arena, offsets, full,
-                               status);
-            tile0 = full;
-        }
+        const uint64_t tile0 = 0;
         const uint64_t rest = (n + T - 1) / T - tile0;
         if (rest) {
             auto k1 = B < 128 ? (s->ext ? k_decode_fixed8<true> : k_decode_fixed8<false>)

@@ -48,14 +48,8 @@ struct Tune {
     bool sizes_scan = false;
     bool decode_generic = false;
     int dec_tile_bytes = 0;      // 0: 24 KB for B >= 128, else 16 KB
-    int dec_persist = 0;         // fixed-layout decode, persistent double-buffered workgroups
-                                 // (k_decode_fixed_p, measured slower: M 0.098 -> 0.157 ms):
-                                 // 0 off, 1 when there are >= 2 full tiles per CU, 2 always
-    int dec_persist_grid = 0;    // > 0: at most this many persistent workgroups (tests)
     bool dec_w16 = true;         // PACKOS_DEC_W16=0: the fixed decoder's dword path for 16k-byte columns too
     int enc_flat = 2;            // PACKOS_ENC_FLAT: 0 never, 1 always, 2 auto (large blobs)
-    int flat_gl = 0;             // PACKOS_FLAT_GL: lanes per blob of the streaming pass (8 / 16 / 64; 0 = by blob size)
-    int flat_w = 0;              // PACKOS_FLAT_W: streaming flat encoder, var bytes per window (0: the chunk-gather kernel)
 };
 
 struct DeviceTables {

@@ -68,7 +68,7 @@ def rows(chain, n, seed, lens=LENS):
     return [[value(rng, s, lens) for s in chain.Schemas] for _ in range(n)]
 
 
-def check(chain, hc, mode, what, shift=False, off64=False, kernel=None):
+def check(chain, hc, mode, what, shift=False, off64=False, kernel=None, cap_scale=1, flags=0):
     T = torch()
     s = CompiledSchema(chain, mode)
     dc = DeviceColumns.from_host(s, hc, "cuda:0")
@@ -89,11 +89,11 @@ def check(chain, hc, mode, what, shift=False, off64=False, kernel=None):
     a0, o0, s0 = ob.encode(chain, hc, mode, nthreads=8)
     n = hc.n
     L = _lib.lib()
-    out = T.zeros(int(o0[n]) + 16, dtype=T.uint8, device="cuda:0")
+    out = T.zeros(int(o0[n]) * cap_scale + 16, dtype=T.uint8, device="cuda:0")
     offs = T.full((n + 1,), -1, dtype=T.int64, device="cuda:0")
     st = T.full((n,), -1, dtype=T.int32, device="cuda:0")
     assert L.packos_encode_batch(s.handle, arr, n, out.data_ptr(), out.numel(), offs.data_ptr(), st.data_ptr(),
-                                 None, 0, 0, None) == 0, L.packos_last_error()
+                                 None, 0, flags, None) == 0, L.packos_last_error()
     T.cuda.synchronize()
     if kernel:   # the encoder under test actually ran (not a silent fallback)
         ok = (kernel,) if isinstance(kernel, str) else kernel
@@ -108,19 +108,10 @@ def check(chain, hc, mode, what, shift=False, off64=False, kernel=None):
     assert np.array_equal(st.cpu().numpy().astype(np.uint32), s0), f"{what}: status differs"
 
 
-# (PACKOS_FLAT_W, PACKOS_FLAT_GL): the streaming kernel's window bytes
-# (default 12288; 64 cuts nearly every blob across windows; 0 = the
-# chunk-gather kernel) and lanes per blob (0 = by mean blob size, 8 / 16 lane
-# groups, 64 a wave per blob)
-FLAT_VARIANTS = [("8192", "0"), ("0", "0"), ("64", "64"), ("8192", "8"), ("4096", "16"), ("64", "8")]
-
-
-@pytest.fixture(autouse=True, params=FLAT_VARIANTS, ids=lambda p: f"W{p[0]}-GL{p[1]}")
-def flat_on(request, monkeypatch):
+@pytest.fixture(autouse=True)
+def flat_on(monkeypatch):
     monkeypatch.setenv("PACKOS_ENC_FLAT", "1")   # read when the schema compiles
-    monkeypatch.setenv("PACKOS_FLAT_W", request.param[0])
-    monkeypatch.setenv("PACKOS_FLAT_GL", request.param[1])
-    return "flat" if request.param[0] == "0" else "flat_s"
+    return "flat"
 
 
 @pytest.mark.parametrize("seed", range(40))
@@ -129,10 +120,7 @@ def test_flat_random_flat(seed, flat_on):
     chain = flat_chain(rng)
     n = [1, 127, 128, 129, 300, 1000, 2049][seed % 7]
     hc = HostColumns.from_rows(chain, rows(chain, n, seed * 11 + 5))
-    # a wide static image leaves the streaming pass too little LDS for even a
-    # 1-KiB window: the chunk-gather pass then takes the chain
-    want = flat_on if flat_on == "flat" else ("flat_s", "flat")
-    check(chain, hc, seed % 2, f"seed {seed}", shift=seed % 3 == 1, off64=seed % 4 == 3, kernel=want)
+    check(chain, hc, seed % 2, f"seed {seed}", shift=seed % 3 == 1, off64=seed % 4 == 3, kernel=flat_on)
 
 
 def test_flat_wide_fixed_leaf_falls_back():
@@ -188,3 +176,18 @@ def test_flat_capacity_overrun():
         last = int(o0[int(fits.sum())])
         assert np.array_equal(out.cpu().numpy()[:last], a0[:last])
         assert np.array_equal(offs.cpu().numpy().astype(np.uint64), o0)
+
+
+@pytest.mark.parametrize("name,cap_scale,flags,want", [
+    ("C5", 1, 0, "flat"), ("C5", 3, 0, "flat"), ("C5", 1, 4, "flat"),
+    ("C3", 1, 0, "tiles"), ("C3", 4, 0, "tiles"), ("C3", 1, 4, "tiles"),
+    # C3 with a capacity of 4x its size, declared exact: the caller's word is taken
+    ("C3", 4, 4, "flat")])
+def test_flat_auto_dispatch(name, cap_scale, flags, want, monkeypatch):
+    """PACKOS_ENC_FLAT unset: the flat / tiles choice follows the batch's mean
+    blob size (static bytes + var bytes read back from the offsets), not the
+    arena the caller passed; PACKOS_ENC_CAP_EXACT (4) takes out_capacity / n."""
+    monkeypatch.delenv("PACKOS_ENC_FLAT", raising=False)
+    cfg = CONFIGS[name]
+    hc = make_columns(cfg, n=3000)
+    check(cfg.chain, hc, 0, f"{name} x{cap_scale} flags {flags}", kernel=want, cap_scale=cap_scale, flags=flags)

@@ -447,19 +447,6 @@ def test_empty_batch_and_empty_chain():
 
 
 # --------------------------------------------------------------- decode ----
-# persistent fixed decode (k_decode_fixed_p): "auto" takes it only for >= 2
-# full tiles per CU (none of these batches); "force" takes it for every full
-# tile with at most 5 workgroups, so each walks many tiles through both buffers
-PERSIST = {"auto": (None, None), "force": ("2", "5")}
-
-
-def _persist_env(monkeypatch, mode):
-    p, g = PERSIST[mode]
-    if p:
-        monkeypatch.setenv("PACKOS_DEC_PERSIST", p)
-        monkeypatch.setenv("PACKOS_DEC_PERSIST_GRID", g)
-
-
 def gpu_decode(chain, arena_np, offs_np, n, stride=0):
     T = torch()
     s = CompiledSchema(chain, 0)
@@ -635,16 +622,13 @@ class _RawDevBuf:
         self.hip.hipFree(C.c_void_p(self.base))
 
 
-@pytest.mark.parametrize("persist", list(PERSIST))
 @pytest.mark.parametrize("cfg,seed", [("M", 0), ("M", 1), ("C1", 2)])
-def test_decode_fixed_truncated_exact_alloc(cfg, seed, persist, monkeypatch):
+def test_decode_fixed_truncated_exact_alloc(cfg, seed):
     """A fixed-schema batch whose blobs are truncated (end offsets pulled
     inward) decoded from an arena that ends exactly at the end of its
     allocation, on a page boundary: the fixed-layout tile staging must stop
     at the tile's last offset, and statuses match the oracle (tiles with a
-    truncated blob are not contiguous: the per-blob path, in the one-shot and
-    the persistent kernel)."""
-    _persist_env(monkeypatch, persist)
+    truncated blob are not contiguous: the per-blob path)."""
     T = torch()
     rng = np.random.default_rng(seed)
     c = CONFIGS[cfg]
@@ -723,19 +707,17 @@ def test_fixed_decode_fast_path(seed):
 
 
 
-@pytest.mark.parametrize("persist", list(PERSIST))
 @pytest.mark.parametrize("tile", [None, "1024", "49152"], ids=["tile_default", "tile_1k", "tile_48k"])
 @pytest.mark.parametrize("B", [32, 64, 128, 256, 512, 1024, 48, 272])
-def test_fixed_decode_blob_sizes(B, tile, persist, monkeypatch):
+def test_fixed_decode_blob_sizes(B, tile, monkeypatch):
     """k_decode_fixed across blob sizes (power-of-two 32..1024 B and two
     others; tile T = 16 * floor(1024 / B) blobs): narrow columns (int16 /
     bool / int32 / int64) next to a string filling the blob, a ragged last
     tile, corrupted blobs in the mix, offsets and stride addressing; decode
     tiles of 1 KB / 48 KB staged bytes (PACKOS_DEC_TILE_BYTES) besides the
-    default; one-shot and persistent tiles."""
+    default."""
     if tile:
         monkeypatch.setenv("PACKOS_DEC_TILE_BYTES", tile)
-    _persist_env(monkeypatch, persist)
     L = B - 2 * 6 - (2 + 1 + 4 + 8)
     chain = SChain(SInt16, SBool, SInt32, SInt64, SStringLen(L))
     s = CompiledSchema(chain, 0)
@@ -756,12 +738,10 @@ def test_fixed_decode_blob_sizes(B, tile, persist, monkeypatch):
 
 
 @pytest.mark.parametrize("seed", range(10))
-def test_fixed_decode_persistent(seed, monkeypatch):
-    """k_decode_fixed_p on random fixed schemas: in-place corruption (check
+def test_fixed_decode_random_gap(seed):
+    """k_decode_fixed on random fixed schemas: in-place corruption (check
     failures inside contiguous tiles), a gap between two blobs (one tile not
-    contiguous), offsets and stride addressing, 1..7 workgroups."""
-    monkeypatch.setenv("PACKOS_DEC_PERSIST", "2")
-    monkeypatch.setenv("PACKOS_DEC_PERSIST_GRID", str(1 + seed % 7))
+    contiguous), offsets and stride addressing."""
     rng = np.random.default_rng(5000 + seed)
     chain = rand_chain(seed + 100, allow_var=False, allow_null=False)
     s = CompiledSchema(chain, 0)
@@ -776,9 +756,9 @@ def test_fixed_decode_persistent(seed, monkeypatch):
         a, b = int(offs[i]), int(offs[i + 1])
         if b > a:
             arena[a + int(rng.integers(0, b - a))] ^= np.uint8(1 << int(rng.integers(0, 8)))
-    st = assert_same_decode(chain, arena, offs, n, f"persist offs seed {seed}")
+    st = assert_same_decode(chain, arena, offs, n, f"fixed offs seed {seed}")
     if np.all(np.diff(offs.astype(np.int64)) == B):
-        st2 = assert_same_decode(chain, arena, offs, n, f"persist stride seed {seed}", stride=B)
+        st2 = assert_same_decode(chain, arena, offs, n, f"fixed stride seed {seed}", stride=B)
         assert np.array_equal(st, st2)
     # 16 zero bytes between blobs g - 1 and g: g's tile is not contiguous
     g = int(rng.integers(1, n))
@@ -786,7 +766,7 @@ def test_fixed_decode_persistent(seed, monkeypatch):
     arena2 = np.concatenate([arena[:cut], np.zeros(16, np.uint8), arena[cut:]])
     offs2 = offs.astype(np.uint64).copy()
     offs2[g:] += np.uint64(16)
-    assert_same_decode(chain, arena2, offs2, n, f"persist gap seed {seed}")
+    assert_same_decode(chain, arena2, offs2, n, f"fixed gap seed {seed}")
 
 
 @pytest.mark.parametrize("name", ["M", "C2", "C4"])
