@@ -48,10 +48,13 @@ def parse():
     p.add_argument("--config", default="M")
     p.add_argument("--blobs-per-gpu", type=int, default=0, help="blobs per GPU (default: the config's shard)")
     p.add_argument("--sets", type=int, default=3, help="device copies rotated in the timed loop (cold)")
+    p.add_argument("--passes", type=int, default=3,
+                   help="timed cold passes (the headline is their median); warm passes interleave between them")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline / parity leg")
     p.add_argument("--no-host", action="store_true", help="skip the host-resident library leg")
     p.add_argument("--no-warm", action="store_true", help="skip the warm (single-set) loop, e.g. for PMC passes")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--parity-piece", type=int, default=1 << 20, help="N > 1: blobs per piece of the shard parity check")
     p.add_argument("--op", default="encode", choices=["encode", "decode", "get"],
                    help="decode: schema.DecodeBuffer over the encoded shard; get: GetAccess GetInt of "
                         "top-level field --get-pos with the typed gather (per-config tables, not the metric)")
@@ -115,6 +118,46 @@ def first_int64(chain):
         if node.kind == "int" and node.width == 8:
             return j
     return 0
+
+
+# ----------------------------------------------------------------- provenance
+PRODUCT_FILES = ("packos_amd/csrc", "include/packos.h", "__graft_entry__.py")
+
+
+def product_tree_hash():
+    """sha256 (16 hex) over the product sources libpackos.so is built from
+    (packos_amd/csrc/*, include/packos.h, the build line in __graft_entry__.py):
+    a PMC summary measured on a tree with the same hash measured this code."""
+    h = hashlib.sha256()
+    for rel in PRODUCT_FILES:
+        path = os.path.join(ROOT, rel)
+        files = sorted(os.path.join(path, f) for f in os.listdir(path)) if os.path.isdir(path) else [path]
+        for f in files:
+            if os.path.isfile(f):
+                h.update(os.path.relpath(f, ROOT).encode() + b"\0")
+                with open(f, "rb") as fh:
+                    h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(config, op):
+    """HBM bytes per launch from bench_pmc/pmc_<config>[_<op>].json (separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench command,
+    summarised by tools/pmc_summary.py), reported only when that summary's
+    product-tree hash equals this tree's."""
+    name = f"pmc_{config}.json" if op == "encode" else f"pmc_{config}_{op}.json"
+    path = os.path.join(ROOT, "bench_pmc", name)
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        pmc = json.load(f)
+    here = product_tree_hash()
+    if pmc.get("product_tree") != here:
+        return None, f"bench_pmc/{name} is stale: product tree {pmc.get('product_tree')} != this tree's {here}"
+    return pmc.get("hbm_bytes_per_launch"), (
+        f"bench_pmc/{name}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE of kernel {pmc.get('kernel', '?')[:60]}, "
+        f"measured at commit {pmc.get('commit', '?')} on product tree {here} (= this tree's); "
+        f"traffic / algorithmic = {pmc.get('traffic_over_algorithmic')}")
 
 
 # ----------------------------------------------------------------- host info
@@ -190,33 +233,39 @@ def cpu_leg(cfg, hc, seconds, gpu_arena, gpu_offsets):
     return res, hi, same, digest, total
 
 
-def shard_parity(cfg, hc, gpu_arena, gpu_offsets, threads, max_blobs=1 << 21):
-    """One oracle encode of this rank's slice (its first `max_blobs` blobs
-    when the shard is larger: a C5 shard is 8 GB), compared with its GPU
-    output."""
+def shard_parity(cfg, hc, out_dev, offs_dev, blob_size, threads, piece=1 << 20):
+    """This rank's whole shard vs the CPU oracle, piece by piece (a C5 shard
+    is 8 GB: each piece's GPU bytes come to the host, the oracle encodes the
+    same rows, compare, free).  Returns (same, checked blobs, digest)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_bridge as ob  # checker only
-    if hc.n > max_blobs:
-        from packos_amd.shard import slice_columns
-        m = max_blobs
-        if gpu_offsets is not None:
-            gpu_arena, gpu_offsets = gpu_arena[: int(gpu_offsets[m])], gpu_offsets[: m + 1]
-        else:   # fixed size: blob i at i * B
-            gpu_arena = gpu_arena[: m * (len(gpu_arena) // hc.n)]
-        hc = slice_columns(hc, 0, m)
-    os_ = ob.OracleSchema(cfg.chain)
-    keep = []
-    cols = ob.make_cols(hc, keep)
+    from packos_amd.shard import slice_columns
     n = hc.n
-    total = int(gpu_offsets[n]) if gpu_offsets is not None else len(gpu_arena)
-    arena = np.empty(max(total, 1), np.uint8)
-    offs = np.empty(n + 1, np.uint64)
-    r = ob.lib().or_encode_batch(ob.C.byref(os_.s), cols, n, cfg.mode, arena.ctypes.data, arena.size,
-                                 offs.ctypes.data, None, threads)
-    same = r == total and bool(np.array_equal(arena[:total], gpu_arena[:total]))
-    if gpu_offsets is not None:
-        same = same and bool(np.array_equal(offs, gpu_offsets.astype(np.uint64)))
-    return same, hashlib.sha256(gpu_arena[:total].tobytes()).hexdigest()[:16]
+    offs_all = None if offs_dev is None else offs_dev[: n + 1].cpu().numpy().astype(np.uint64)
+    h = hashlib.sha256()
+    same, checked = True, 0
+    for a in range(0, n, piece):
+        b = min(n, a + piece)
+        if offs_all is not None:
+            a0, b0 = int(offs_all[a]), int(offs_all[b])
+        else:
+            a0, b0 = a * blob_size, b * blob_size
+        g = out_dev[a0:b0].cpu().numpy()
+        sub = slice_columns(hc, a, b)
+        os_ = ob.OracleSchema(cfg.chain)
+        keep = []
+        cols = ob.make_cols(sub, keep)
+        arena = np.empty(max(b0 - a0, 1), np.uint8)
+        offs = np.empty(b - a + 1, np.uint64)
+        r = ob.lib().or_encode_batch(ob.C.byref(os_.s), cols, b - a, cfg.mode, arena.ctypes.data, arena.size,
+                                     offs.ctypes.data, None, threads)
+        same = same and r == b0 - a0 and bool(np.array_equal(arena[: b0 - a0], g))
+        if offs_all is not None:
+            same = same and bool(np.array_equal(offs, offs_all[a: b + 1] - np.uint64(a0)))
+        h.update(g.tobytes())
+        checked += b - a
+        del g, arena, sub, keep
+    return same, checked, h.hexdigest()[:16]
 
 
 def decode_parity(cfg, arena, offsets, stride, n, gout, gst, threads):
@@ -259,11 +308,13 @@ def get_parity(arena, offsets, stride, n, path, getter, gvals, gst):
     return same, int(ok.sum()), hashlib.sha256(g_vals.tobytes() + g_st.tobytes()).hexdigest()[:16]
 
 
-def pcie_ceiling(dev, nbytes=256 << 20, reps=4, piece=64 << 20):
+def pcie_ceiling(dev, nbytes=256 << 20, repeats=3, pieces=(4 << 20, 16 << 20, 64 << 20)):
     """Pinned host <-> device copy rates of this box (GB/s) with plain HIP
     calls (libamdhip64 through ctypes): H2D alone, D2H alone, and both at once
-    on two streams in `piece`-byte copies (the full-duplex ceiling a pipelined
-    host batch can reach; `bidir_total_gbs` = both directions' bytes / time)."""
+    on two streams, each the BEST over `repeats` runs at every copy size in
+    `pieces` (the host pipeline moves 4-64 MiB chunks, three in flight), so the
+    ceiling is the link's, not one copy shape's.  `bidir_total_gbs` = both
+    directions' bytes / time."""
     import ctypes as C
     import torch
     torch.cuda.synchronize()
@@ -285,30 +336,35 @@ def pcie_ceiling(dev, nbytes=256 << 20, reps=4, piece=64 << 20):
         return {"error": "HIP allocation failed"}
     H2D, D2H = 1, 2
 
-    def run(h2d, d2h):
+    def run(h2d, d2h, piece):
         hip.hipStreamSynchronize(s1)
         hip.hipStreamSynchronize(s2)
         t0 = time.perf_counter()
-        for _ in range(reps):
-            for off in range(0, nbytes, piece):
-                if h2d:
-                    hip.hipMemcpyAsync(vp(d_in.value + off), vp(h_in.value + off), piece, H2D, s1)
-                if d2h:
-                    hip.hipMemcpyAsync(vp(h_out.value + off), vp(d_out.value + off), piece, D2H, s2)
+        for off in range(0, nbytes, piece):
+            if h2d:
+                hip.hipMemcpyAsync(vp(d_in.value + off), vp(h_in.value + off), piece, H2D, s1)
+            if d2h:
+                hip.hipMemcpyAsync(vp(h_out.value + off), vp(d_out.value + off), piece, D2H, s2)
         hip.hipStreamSynchronize(s1)
         hip.hipStreamSynchronize(s2)
-        return nbytes * reps * (int(h2d) + int(d2h)) / (time.perf_counter() - t0) / 1e9
-    run(True, True)
-    h2d, d2h, both = run(True, False), run(False, True), run(True, True)
+        return nbytes * (int(h2d) + int(d2h)) / (time.perf_counter() - t0) / 1e9
+    run(True, True, pieces[-1])
+    best = {"h2d": 0.0, "d2h": 0.0, "both": 0.0}
+    for piece in pieces:
+        for _ in range(repeats):
+            best["h2d"] = max(best["h2d"], run(True, False, piece))
+            best["d2h"] = max(best["d2h"], run(False, True, piece))
+            best["both"] = max(best["both"], run(True, True, piece))
     for p_ in (d_in, d_out):
         hip.hipFree(p_)
     for p_ in (h_in, h_out):
         hip.hipHostFree(p_)
     hip.hipStreamDestroy(s1)
     hip.hipStreamDestroy(s2)
-    return {"h2d_gbs": round(h2d, 2), "d2h_gbs": round(d2h, 2), "bidir_total_gbs": round(both, 2),
-            "note": f"hipMemcpyAsync of pinned (hipHostMalloc) {nbytes >> 20} MiB x {reps} in {piece >> 20} MiB pieces; "
-                    "bidir = H2D and D2H on two streams at once, both directions' bytes / time"}
+    return {"h2d_gbs": round(best["h2d"], 2), "d2h_gbs": round(best["d2h"], 2), "bidir_total_gbs": round(best["both"], 2),
+            "note": f"hipMemcpyAsync of pinned (hipHostMalloc) {nbytes >> 20} MiB in "
+                    f"{'/'.join(str(p >> 20) for p in pieces)} MiB copies, best of {repeats} per size; bidir = H2D "
+                    "and D2H on two streams at once, both directions' bytes / time"}
 
 
 def pcie_time(pcie, b_in, b_out):
@@ -516,11 +572,41 @@ def main():
             el = float(t.item())
         return el, ev0.elapsed_time(ev1) / steps
 
-    # the headline (cold, rotated sets) first, the warm replay after it: a warm
-    # pass run first left M decode's cold number ~10 % higher in the same
-    # process (0.108 vs 0.098 ms, round 4), the kernel unchanged
-    el, kernel_ms = timed(runs, args.steps, args.warmup)
-    warm_el, warm_kms = (None, None) if args.no_warm else timed(runs[:1], args.steps, args.warmup)
+    # Every timed pass starts from a scrubbed cache: a 512 MiB write evicts the
+    # L2s and the 256 MiB Infinity Cache (MALL), so no pass inherits another's
+    # lines.  Cold passes (rotated sets) and warm passes (set 0 replayed)
+    # interleave, cold first and last (cold, warm, cold, warm, cold for 3
+    # passes): the headline is the median cold pass, and the spread over the
+    # passes, in both orders, is reported.
+    scrub_buf = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+
+    def scrub(k):
+        scrub_buf.fill_(k & 0xFF)
+        torch.cuda.synchronize()
+
+    order = []
+    for k in range(max(1, args.passes)):
+        order.append("cold")
+        if not args.no_warm and k + 1 < max(1, args.passes):
+            order.append("warm")
+    if not args.no_warm and args.passes <= 1:
+        order.append("warm")
+    passes = []
+    for k, kind in enumerate(order):
+        scrub(k)
+        e, km = timed(runs if kind == "cold" else runs[:1], args.steps, args.warmup)
+        passes.append({"kind": kind, "kernel_ms": round(km, 5), "ms_per_step": round(e / args.steps * 1e3, 4),
+                       "_el": e})
+    colds = sorted((p for p in passes if p["kind"] == "cold"), key=lambda p: p["kernel_ms"])
+    warms = sorted((p for p in passes if p["kind"] == "warm"), key=lambda p: p["kernel_ms"])
+    mid = colds[(len(colds) - 1) // 2]
+    el, kernel_ms = mid["_el"], mid["kernel_ms"]
+    warm_el, warm_kms = (None, None) if not warms else (warms[(len(warms) - 1) // 2]["_el"],
+                                                       warms[(len(warms) - 1) // 2]["kernel_ms"])
+    for p_ in passes:
+        del p_["_el"]
+    cold_spread = (colds[-1]["kernel_ms"] - colds[0]["kernel_ms"]) / kernel_ms if kernel_ms else 0.0
+    del scrub_buf
 
     alg = algorithmic_bytes(hc, total_out, with_offsets=not fixed)
     gran = None   # granularity-aware bytes: reads counted as whole 128-B lines
@@ -560,23 +646,9 @@ def main():
     warm_achieved = alg / (warm_kms * 1e-3) / 1e9 if warm_kms else None
 
     # PMC traffic is not collected in this process (rocprofv3 --pmc runs are
-    # separate passes of this same command); the summary of such a pass, with
-    # its provenance, is read from profiles/ when present.
-    traffic, traffic_src = None, None
-    pmc_name = f"pmc_{args.config}.json" if args.op == "encode" else f"pmc_{args.config}_{args.op}.json"
-    for rnd in ("r04", "r03", "r02"):
-        pmc_path = os.path.join(ROOT, "profiles", rnd, pmc_name)
-        if not os.path.exists(pmc_path):
-            continue
-        try:
-            with open(pmc_path) as f:
-                pmc = json.load(f)
-            traffic = pmc.get("hbm_bytes_per_launch")
-            traffic_src = (f"profiles/{rnd}/{pmc_name}, measured at commit {pmc.get('commit', 'unstamped')}: "
-                           f"{pmc.get('source', '')}")
-        except Exception:
-            traffic = None
-        break
+    # separate passes of this same command): bench_pmc/ holds their summary,
+    # used when it was measured on this same product tree.
+    traffic, traffic_src = pmc_traffic(args.config, args.op)
 
     cpu, parity, host = None, None, None
     if args.op != "encode":
@@ -598,20 +670,22 @@ def main():
         parity = {"result": "bit-exact" if same else "MISMATCH", "blobs": n, "bytes": tot,
                   "sha256_16": digest, "checked": "GPU arena of the timed run vs the CPU oracle, whole shard"}
     if world > 1 and not args.no_cpu and args.op == "encode":
-        # every rank checks its own shard against the CPU oracle's encoding of
-        # the same slice (SCALE runs carry correctness); flags meet in a MIN
-        gpu_arena = sets[0].out[:total_out].cpu().numpy()
-        gpu_offs = None if fixed else sets[0].offsets.cpu().numpy()
+        # every rank checks its WHOLE shard against the CPU oracle's encoding of
+        # the same global slice, piece by piece (SCALE runs carry the same
+        # correctness as the 1-GPU line); flags meet in a MIN
         hi_ = host_info()
         th = max(1, (int(hi_["cgroup_cpu_quota"] or 0) or hi_["affinity"] or 1) // max(1, int(
             os.environ.get("LOCAL_WORLD_SIZE", world))))
-        same, digest = shard_parity(cfg, hc, gpu_arena, gpu_offs, th)
-        flag = torch.tensor([1 if same else 0], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        parity = {"result": "bit-exact" if int(flag.item()) == 1 else "MISMATCH", "ranks": world,
-                  "blobs_rank0": n, "checked_blobs_per_rank": min(n, 1 << 21), "sha256_16_rank0": digest,
-                  "checked": "every rank: its GPU shard (its first 2M blobs when larger) vs the CPU oracle's "
-                             "encoding of the same global slice"}
+        same, checked, digest = shard_parity(cfg, hc, sets[0].out, None if fixed else sets[0].offsets,
+                                             schema.fixed_blob_size, th, piece=max(1, args.parity_piece))
+        flag = torch.tensor([1 if same and checked == n else 0, checked], dtype=torch.int64,
+                            device=dev if backend == "nccl" else "cpu")
+        mins = flag.clone()
+        dist.all_reduce(mins, op=dist.ReduceOp.MIN)
+        parity = {"result": "bit-exact" if int(mins[0].item()) == 1 else "MISMATCH", "ranks": world,
+                  "blobs_rank0": n, "checked_blobs_per_rank_min": int(mins[1].item()), "sha256_16_rank0": digest,
+                  "checked": "every rank: its whole GPU shard (in 1M-blob pieces) vs the CPU oracle's encoding of "
+                             "the same global slice"}
     if args.op != "encode" and os.environ.get("PACKOS_BENCH_NO_PARITY") is None:
         # the timed run's set-0 outputs vs the CPU oracle over this rank's whole
         # shard (every rank; flags meet in a MIN)
@@ -675,7 +749,11 @@ def main():
                              "frac_granularity": round(gran / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                              "granularity_rule": f"reads counted as whole {LINE}-B lines (union over blobs)"}),
                          "cache_state": f"cold: {len(sets)} sets rotated ({footprint / 2 ** 20:.0f} MiB > 256 MiB "
-                                        "Infinity Cache)"},
+                                        "Infinity Cache), every pass after a 512 MiB scrub write"},
+            "passes": {"order": [p_["kind"] for p_ in passes], "kernel_ms": [p_["kernel_ms"] for p_ in passes],
+                       "ms_per_step": [p_["ms_per_step"] for p_ in passes],
+                       "cold_spread": round(cold_spread, 4),
+                       "headline": "median cold pass (each pass: W warmup + exactly K timed steps)"},
             "warm": None if warm_kms is None else {
                 "kernel_ms": round(warm_kms, 5), "achieved": round(warm_achieved, 1),
                 "frac": round(warm_achieved / HBM_PEAK_GBS, 4), "ms_per_step": round(warm_el / args.steps * 1e3, 4),

@@ -90,7 +90,7 @@ def test_bench_two_ranks_rehearsal():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--config", "C5", "--blobs-per-gpu", "20000", "--steps", "3", "--warmup", "1", "--sets", "1",
-           "--no-host", "--no-warm"]
+           "--no-host", "--no-warm", "--parity-piece", "7000"]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -99,3 +99,6 @@ def test_bench_two_ranks_rehearsal():
     assert line["n_gpus"] == 2 and line["config"]["global_blobs"] == 40000 and line["value"] > 0
     # every rank checked its shard against the oracle's encoding of its slice
     assert line["parity"]["result"] == "bit-exact" and line["parity"]["ranks"] == 2
+    # ... its WHOLE shard, in 7000-blob pieces (a flag per rank: all pieces, all blobs)
+    assert line["parity"]["checked_blobs_per_rank_min"] > 14000
+    assert len(line["passes"]["order"]) == 3 and set(line["passes"]["order"]) == {"cold"}

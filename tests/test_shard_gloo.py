@@ -143,3 +143,51 @@ def test_streamed_plan_matches_full_plan(cfg_name, per_gpu, world, piece):
     full = plan_shards(sizes, world)
     got = [config_shard(cfg, s, per_gpu, world, r, piece=piece)[:2] for r in range(world)]
     assert got == [tuple(x) for x in full]
+
+
+def _parity_worker(rank, world, port, cfg_name, n, piece, q):
+    """bench.shard_parity on each rank's shard (CPU tensors stand in for the
+    device arena) and the MIN-reduced flag bench.py builds from it."""
+    import sys
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = CONFIGS[cfg_name]
+    schema = CompiledSchema(cfg.chain, cfg.mode)
+    hc = make_columns(cfg, n=n)
+    lo, hi = plan_shards(blob_sizes_host(schema, hc), world)[rank]
+    mine = slice_columns(hc, lo, hi)
+    arena, offs, _ = ob.encode(cfg.chain, mine, cfg.mode)
+    fixed = schema.fixed_blob_size > 0
+    out = torch.from_numpy(arena.copy())
+    od = None if fixed else torch.from_numpy(offs.astype(np.int64))
+    same, checked, _ = bench.shard_parity(cfg, mine, out, od, schema.fixed_blob_size, 2, piece=piece)
+    # one corrupted byte in the rank's last piece must be caught
+    out[-1] ^= 0xFF
+    bad, _, _ = bench.shard_parity(cfg, mine, out, od, schema.fixed_blob_size, 2, piece=piece)
+    flag = torch.tensor([1 if same and checked == hi - lo else 0, checked], dtype=torch.int64)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    q.put((rank, same, bad, checked, hi - lo, int(flag[0]), int(flag[1])))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg_name,n,piece", [("C5", 3000, 700), ("M", 2048, 1000), ("C3", 4000, 1 << 20)])
+def test_two_rank_whole_shard_parity(cfg_name, n, piece):
+    """bench.py's N > 1 encode parity covers each rank's WHOLE shard in
+    pieces (round 4 capped it at the first 2M blobs)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_parity_worker, args=(r, 2, port, cfg_name, n, piece, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, same, bad, checked, rows, f0, f1 in res:
+        assert same and not bad and checked == rows
+        assert f0 == 1 and f1 == min(r[4] for r in res)

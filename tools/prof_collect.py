@@ -10,7 +10,10 @@ bytes per launch (FETCH_SIZE and WRITE_SIZE are KiB; fetch reported raw and
 with MI355X_MICROARCH.md's gfx950 x2 for 16-B/lane streaming reads, the
 factor measured by tools/fetch_calib.hip for scattered shapes is applied when
 given in calib.json), and the SQ counters per wave.  Also writes
-profiles/<round>/pmc_<cfg>[_<op>].json, which bench.py reads for `traffic`.
+profiles/<round>/pmc_<cfg>[_<op>].json and bench_pmc/pmc_<cfg>[_<op>].json,
+which bench.py reads for `traffic` when its product_tree (the hash
+tools/prof_ops.sh recorded on the box, bench.product_tree_hash) equals the
+running tree's.
 """
 import csv
 import glob
@@ -64,6 +67,12 @@ def main():
     if os.path.exists(cpath):
         calib = json.load(open(cpath))
     out = []
+    tree = None
+    tpath = os.path.join(src, "product_tree.txt")
+    if os.path.exists(tpath):
+        tree = open(tpath).read().strip() or None
+    bench_pmc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench_pmc")
+    os.makedirs(bench_pmc, exist_ok=True)
     for line_log in sorted(glob.glob(os.path.join(src, "*.line.log"))):
         tag = os.path.basename(line_log)[: -len(".line.log")]
         cfg, op = tag.rsplit("_", 1)
@@ -113,7 +122,8 @@ def main():
             res["traffic_over_algorithmic"] = round(res["hbm_bytes_per_launch"] / res["algorithmic_bytes_per_launch"], 4)
             if res.get("granularity_bytes_per_launch"):
                 res["traffic_over_granularity"] = round(res["hbm_bytes_per_launch"] / res["granularity_bytes_per_launch"], 4)
-            pmc = {"kernel": kname, "commit": commit, "hbm_bytes_per_launch": res["hbm_bytes_per_launch"],
+            pmc = {"kernel": kname, "commit": commit, "product_tree": tree,
+                   "hbm_bytes_per_launch": res["hbm_bytes_per_launch"],
                    "fetch_bytes_per_launch": res["fetch_bytes_raw"] * fac, "write_bytes_per_launch": res["write_bytes"],
                    "algorithmic_bytes_per_launch": res["algorithmic_bytes_per_launch"],
                    "traffic_over_algorithmic": res["traffic_over_algorithmic"],
@@ -122,8 +132,9 @@ def main():
                    "source": f"{dst}/{tag}_pmc_fetch_size.csv, {dst}/{tag}_pmc_write_size.csv "
                              "(rocprofv3 --pmc, separate passes)"}
             name = f"pmc_{cfg}.json" if op == "encode" else f"pmc_{cfg}_{op}.json"
-            with open(os.path.join(rnd_dir, name), "w") as f:
-                json.dump(pmc, f, indent=1)
+            for d in (rnd_dir, bench_pmc):
+                with open(os.path.join(d, name), "w") as f:
+                    json.dump(pmc, f, indent=1)
         with open(os.path.join(dst, f"{tag}.json"), "w") as f:
             json.dump(res, f, indent=1)
         out.append(res)

@@ -5,11 +5,13 @@
 # Output under gpurun_out/p3/<cfg>_<op>*; tools/prof_collect.py summarises.
 set -u
 R="$GRAFT_REPO_ROOT"; mkdir -p "$R/gpurun_out/p3"
+# the product-tree hash these counters describe (bench.py compares it with its own)
+(cd "$R" && python3 -c "import bench; print(bench.product_tree_hash())") > "$R/gpurun_out/p3/product_tree.txt"
 STEPS=${STEPS:-20}
 SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_ANY SQ_INSTS_VMEM"
 for spec in ${SPECS}; do
   c=${spec%%:*}; op=${spec##*:}; o="$R/gpurun_out/p3/${c}_${op}"
-  B="$R/bench.py --config $c --op $op --no-cpu --no-host ${BARGS:-}"
+  B="$R/bench.py --config $c --op $op --no-cpu --no-host --passes 1 ${BARGS:-}"
   cd "$R"
   echo "$(date +%T) $c $op line"
   timeout -k 10 300 python3 $B --steps $STEPS > "$o.line.log" 2>&1
