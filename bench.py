@@ -55,9 +55,10 @@ def parse():
     p.add_argument("--no-warm", action="store_true", help="skip the warm (single-set) loop, e.g. for PMC passes")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--parity-piece", type=int, default=1 << 20, help="N > 1: blobs per piece of the shard parity check")
-    p.add_argument("--op", default="encode", choices=["encode", "decode", "get"],
-                   help="decode: schema.DecodeBuffer over the encoded shard; get: GetAccess GetInt of "
-                        "top-level field --get-pos with the typed gather (per-config tables, not the metric)")
+    p.add_argument("--op", default="encode", choices=["encode", "decode", "validate", "get"],
+                   help="decode: schema.DecodeBuffer over the encoded shard; validate: schema.ValidateBuffer "
+                        "(status only); get: GetAccess GetInt of top-level field --get-pos with the typed "
+                        "gather (per-config tables, not the metric)")
     p.add_argument("--get-spans", action="store_true",
                    help="--op get: also write start / length / tag (GetInt itself returns only value + error)")
     p.add_argument("--get-pos", type=int, default=-1,
@@ -111,6 +112,45 @@ def static_prefix(chain):
         else:
             pre += w
     return pre, tail_fixed
+
+
+def validate_reads(chain, mode):
+    """(bytes ValidateBuffer reads per all-present blob, window): the header
+    blocks, Match literals and Range / date / prefix / suffix payloads
+    (schema.go:880-891 over the Validate methods), and the leading bytes that
+    hold all of them when none follows a var payload (else None) - the
+    packos_schema val_win rule of compile.cpp."""
+    from packos_amd.schema import CHK_DATE, CHK_MAX, CHK_MIN, CHK_PREFIX, CHK_SUFFIX
+    st = {"pos": 0, "need": 0, "var": False, "after": False, "bytes": 0}
+
+    def item(size, reads, var=False):
+        if var:
+            st["var"] = True
+        if reads:
+            st["bytes"] += size
+            if st["var"]:
+                st["after"] = True
+        if not st["var"]:
+            st["pos"] += size
+            if reads:
+                st["need"] = st["pos"]
+
+    def container(kids):
+        item(2 * (len(kids) + 1) if kids else (2 if mode == 0 else 0), True)
+        for k in kids:
+            node(k)
+
+    def node(x):
+        if x.kind in ("tuple", "map"):
+            container(x.ordered_children())
+        elif x.kind == "match":
+            item(len(x.literal), True)
+        elif x.kind in ("string", "bytes") and x.width <= 0:
+            item(0, bool(x.check & (CHK_PREFIX | CHK_SUFFIX)), var=True)
+        else:
+            item(x.width, bool(x.check & (CHK_MIN | CHK_MAX | CHK_DATE | CHK_PREFIX | CHK_SUFFIX)))
+    container(list(chain.Schemas))
+    return st["bytes"], (None if st["after"] else st["need"])
 
 
 def first_int64(chain):
@@ -293,6 +333,16 @@ def decode_parity(cfg, arena, offsets, stride, n, gout, gst, threads):
                 same = same and bool(np.array_equal(a[:n][ok], b[:n][ok]))
             h.update(np.ascontiguousarray(b[: n * (sp.width if name == "data" else 1)]).tobytes())
     return same, int(ok.sum()), h.hexdigest()[:16]
+
+
+def validate_parity(cfg, arena, offsets, stride, n, gst, threads):
+    """Whole-shard check of a timed ValidateBuffer against the CPU oracle's."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bridge as ob  # checker only
+    o_st = ob.validate(cfg.chain, arena, offsets, n, stride=stride, nthreads=threads, mode=cfg.mode & 0x100)
+    g_st = gst[:n].cpu().numpy().astype(np.uint32)
+    same = bool(np.array_equal(o_st[:n], g_st))
+    return same, int((o_st[:n] == 0).sum()), hashlib.sha256(g_st.tobytes()).hexdigest()[:16]
 
 
 def get_parity(arena, offsets, stride, n, path, getter, gvals, gst):
@@ -521,6 +571,20 @@ def main():
                 return lambda: decode_batch(schema, p.out, None, n, stride=p.B, stream=stream, out=dcols, status=st)
             return lambda: decode_batch(schema, p.out, p.offsets, n, stream=stream, out=dcols, status=st)
         runs = [dec_runner(p) for p in sets]
+    elif args.op == "validate":
+        from packos_amd.api import validate_batch
+        for p in sets:
+            p.run()
+        torch.cuda.synchronize()
+        outs = []
+
+        def val_runner(p):
+            st = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+            outs.append((None, st))
+            if fixed:
+                return lambda: validate_batch(schema, p.out, None, n, stride=p.B, stream=stream, status=st)
+            return lambda: validate_batch(schema, p.out, p.offsets, n, stream=stream, status=st)
+        runs = [val_runner(p) for p in sets]
     elif args.op == "get":
         from packos_amd import _lib
         import ctypes as C
@@ -629,6 +693,13 @@ def main():
         pre, tail_fixed = static_prefix(cfg.chain)
         end = b1 if (pre is None or tail_fixed) else np.minimum(b1, b0 + np.uint64(pre))
         gran = LINE * lines_touched(b0, end) + (0 if fixed else 8 * (n + 1)) + out_b
+    elif args.op == "validate":
+        # ValidateBuffer reads the header blocks, Match literals and checked
+        # payloads (+ the blob offsets for var layouts) and writes the status
+        rb, win = validate_reads(cfg.chain, cfg.mode & 1)
+        alg = n * (rb + 4) + (0 if fixed else 8 * (n + 1))
+        end = b1 if win is None else np.minimum(b1, b0 + np.uint64(win))
+        gran = LINE * lines_touched(b0, end) + n * 4 + (0 if fixed else 8 * (n + 1))
     elif args.op == "get":
         # GetAccess rangeAt: h0 + the two header words around the field + its
         # payload (8 B for an int64) in; GetInt's (value, error) out = value 8 +
@@ -698,6 +769,9 @@ def main():
         if args.op == "decode":
             same, n_ok, digest = decode_parity(cfg, arena_np, offs_np, stride, n, outs[0][0], outs[0][1], th)
             what = "status of every blob + columns / validity / views of every blob that decodes"
+        elif args.op == "validate":
+            same, n_ok, digest = validate_parity(cfg, arena_np, offs_np, stride, n, outs[0][1], th)
+            what = "ValidateBuffer status of every blob"
         else:
             same, n_ok, digest = get_parity(arena_np, offs_np, stride, n, [args.get_pos], 3, outs[0][0], outs[0][1])
             what = "status of every blob + GetInt value of every blob that has one"

@@ -857,7 +857,6 @@ void read_tune(Tune& t) {
     t.decode_generic = getenv("PACKOS_DECODE_GENERIC") != nullptr;
     if (const char* e = getenv("PACKOS_DEC_TILE_BYTES")) t.dec_tile_bytes = std::min(49152, std::max(1024, atoi(e)));
     if (const char* e = getenv("PACKOS_ENC_FLAT")) t.enc_flat = atoi(e);
-    if (const char* e = getenv("PACKOS_DEC_W16")) t.dec_w16 = atoi(e) != 0;
 }
 
 // Same rule as the device's ext_layout_wave (kernels.hip): containers in

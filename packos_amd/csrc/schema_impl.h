@@ -48,7 +48,6 @@ struct Tune {
     bool sizes_scan = false;
     bool decode_generic = false;
     int dec_tile_bytes = 0;      // 0: 24 KB for B >= 128, else 16 KB
-    bool dec_w16 = true;         // PACKOS_DEC_W16=0: the fixed decoder's dword path for 16k-byte columns too
     int enc_flat = 2;            // PACKOS_ENC_FLAT: 0 never, 1 always, 2 auto (large blobs)
 };
 
