@@ -1333,10 +1333,14 @@ __device__ __forceinline__ u32x4 lds16u(const uint8_t* lds, uint32_t q, uint32_t
 __device__ __forceinline__ uint32_t lds_w4(const uint32_t* lds, uint32_t a, uint32_t q) {
     return q ? __builtin_amdgcn_alignbyte(lds[(a >> 2) + 1], lds[a >> 2], q) : lds[a >> 2];
 }
-// dword d (tile column bytes 4d .. 4d + 3) of a column
+// dword d (tile column bytes 4d .. 4d + 3) of a column; KIND: a compile-time
+// kind, or DS_ANY to switch on `kind`
+constexpr uint32_t DS_ANY = 255;
+template <uint32_t KIND = DS_ANY>
 __device__ __forceinline__ uint32_t dfix_dword(const uint32_t* lds, uint32_t kind, uint32_t d, uint32_t w, uint32_t off,
                                                uint32_t magic, uint32_t SB) {
     const uint32_t b = 4 * d, q = off & 3u;
+    if (KIND != DS_ANY) kind = KIND;
     switch (kind) {
         case DS_D4: {    // w % 4 == 0: inside one row
             const uint32_t j = __umulhi(b, magic);
@@ -1382,11 +1386,12 @@ __device__ __forceinline__ u32x4 dfix_unit(const uint32_t* lds, uint32_t kind, u
                                            uint32_t magic, uint32_t SB) {
     const uint32_t q = off & 3u;
     switch (kind) {
-        case DS_G4U: case DS_GENU: {   // four dwords of the column
-            const uint32_t k = kind == DS_G4U ? DS_D4 : DS_GEN;
-            return u32x4{dfix_dword(lds, k, 4 * u, w, off, magic, SB), dfix_dword(lds, k, 4 * u + 1, w, off, magic, SB),
-                         dfix_dword(lds, k, 4 * u + 2, w, off, magic, SB), dfix_dword(lds, k, 4 * u + 3, w, off, magic, SB)};
-        }
+        case DS_G4U:     // four dwords of the column
+            return u32x4{dfix_dword<DS_D4>(lds, 0, 4 * u, w, off, magic, SB), dfix_dword<DS_D4>(lds, 0, 4 * u + 1, w, off, magic, SB),
+                         dfix_dword<DS_D4>(lds, 0, 4 * u + 2, w, off, magic, SB), dfix_dword<DS_D4>(lds, 0, 4 * u + 3, w, off, magic, SB)};
+        case DS_GENU:
+            return u32x4{dfix_dword<DS_GEN>(lds, 0, 4 * u, w, off, magic, SB), dfix_dword<DS_GEN>(lds, 0, 4 * u + 1, w, off, magic, SB),
+                         dfix_dword<DS_GEN>(lds, 0, 4 * u + 2, w, off, magic, SB), dfix_dword<DS_GEN>(lds, 0, 4 * u + 3, w, off, magic, SB)};
         case DS_W8: {    // rows 2u, 2u + 1
             const uint32_t a0 = 2 * u * SB + off, a1 = a0 + SB;
             return u32x4{lds_w4(lds, a0, q), lds_w4(lds, a0 + 4, q), lds_w4(lds, a1, q), lds_w4(lds, a1 + 4, q)};
@@ -1396,15 +1401,15 @@ __device__ __forceinline__ u32x4 dfix_unit(const uint32_t* lds, uint32_t kind, u
             return u32x4{lds_w4(lds, a0, q), lds_w4(lds, a0 + SB, q), lds_w4(lds, a0 + 2 * SB, q),
                          lds_w4(lds, a0 + 3 * SB, q)};
         }
-        case DS_W2: {    // rows 8u .. 8u + 7
-            return u32x4{dfix_dword(lds, DS_D2, 4 * u, w, off, magic, SB), dfix_dword(lds, DS_D2, 4 * u + 1, w, off, magic, SB),
-                         dfix_dword(lds, DS_D2, 4 * u + 2, w, off, magic, SB), dfix_dword(lds, DS_D2, 4 * u + 3, w, off, magic, SB)};
-        }
-        default: {       // DS_W1 / DS_BOOLU: rows 16u .. 16u + 15
-            const uint32_t k = kind == DS_BOOLU ? DS_BOOL : DS_D1;
-            return u32x4{dfix_dword(lds, k, 4 * u, w, off, magic, SB), dfix_dword(lds, k, 4 * u + 1, w, off, magic, SB),
-                         dfix_dword(lds, k, 4 * u + 2, w, off, magic, SB), dfix_dword(lds, k, 4 * u + 3, w, off, magic, SB)};
-        }
+        case DS_W2:      // rows 8u .. 8u + 7
+            return u32x4{dfix_dword<DS_D2>(lds, 0, 4 * u, w, off, magic, SB), dfix_dword<DS_D2>(lds, 0, 4 * u + 1, w, off, magic, SB),
+                         dfix_dword<DS_D2>(lds, 0, 4 * u + 2, w, off, magic, SB), dfix_dword<DS_D2>(lds, 0, 4 * u + 3, w, off, magic, SB)};
+        case DS_BOOLU:   // rows 16u .. 16u + 15
+            return u32x4{dfix_dword<DS_BOOL>(lds, 0, 4 * u, w, off, magic, SB), dfix_dword<DS_BOOL>(lds, 0, 4 * u + 1, w, off, magic, SB),
+                         dfix_dword<DS_BOOL>(lds, 0, 4 * u + 2, w, off, magic, SB), dfix_dword<DS_BOOL>(lds, 0, 4 * u + 3, w, off, magic, SB)};
+        default:         // DS_W1
+            return u32x4{dfix_dword<DS_D1>(lds, 0, 4 * u, w, off, magic, SB), dfix_dword<DS_D1>(lds, 0, 4 * u + 1, w, off, magic, SB),
+                         dfix_dword<DS_D1>(lds, 0, 4 * u + 2, w, off, magic, SB), dfix_dword<DS_D1>(lds, 0, 4 * u + 3, w, off, magic, SB)};
     }
 }
 
@@ -2662,18 +2667,20 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
             bool ok = (B & 3) == 0 && T % 16 == 0;
             for (int c = 0; ok && c < K.n; c++) {
                 const uint32_t w = K.width[c];
-                // LDS read cost per dword (the sort key); 16-B units for blobs
-                // of >= 128 B, lane-interleaved dwords for smaller ones (A/B above)
+                // sort key per dword (the LDS reads and merges a dword takes;
+                // the unit weights measured best for 256-B blobs); 16-B units for
+                // blobs of >= 128 B, lane-interleaved dwords for smaller ones
                 uint32_t kind, cost;
                 const bool q0 = (K.blob_off[c] & 3u) == 0, units = B >= 128;
-                if (w % 16 == 0 && B % 16 == 0) kind = DS_W16, cost = 1;
-                else if (units && w == 8) kind = DS_W8, cost = q0 ? 1 : 2;
-                else if (units && w == 4) kind = DS_W4, cost = q0 ? 1 : 2;
-                else if (w % 4 == 0) kind = units ? DS_G4U : DS_D4, cost = q0 ? 1 : 2;
-                else if (w > 4) kind = units ? DS_GENU : DS_GEN, cost = 3;
-                else if (w == 2) kind = units ? DS_W2 : DS_D2, cost = q0 ? 2 : 4;
-                else if (w == 1) kind = (K.flags[c] & 1u) ? (units ? DS_BOOLU : DS_BOOL) : (units ? DS_W1 : DS_D1), cost = 4;
-                else kind = DS_BYTE, cost = 4;
+                if (w % 16 == 0 && B % 16 == 0) kind = DS_W16, cost = 2;
+                else if (units && w == 8) kind = DS_W8, cost = 4;
+                else if (units && w == 4) kind = DS_W4, cost = 4;
+                else if (w % 4 == 0) kind = units ? DS_G4U : DS_D4, cost = units ? (q0 ? 4 : 8) : (q0 ? 1 : 2);
+                else if (w > 4) kind = units ? DS_GENU : DS_GEN, cost = units ? 10 : 3;
+                else if (w == 2) kind = units ? DS_W2 : DS_D2, cost = units ? 8 : (q0 ? 2 : 4);
+                else if (w == 1) kind = (K.flags[c] & 1u) ? (units ? DS_BOOLU : DS_BOOL) : (units ? DS_W1 : DS_D1),
+                                 cost = units ? 16 : 4;
+                else kind = DS_BYTE, cost = units ? 32 : 4;
                 const uint32_t bytes = T * w;   // whole 16-B units (T % 16 == 0)
                 for (uint32_t blk = 0; 1024u * blk < bytes; blk++) {
                     const uint32_t nd = std::min<uint32_t>(1024u, bytes - 1024u * blk) / 4;
