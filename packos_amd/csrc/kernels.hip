@@ -1521,7 +1521,7 @@ __device__ __forceinline__ void dfix_tile(const DecFixProgram& F, const DecCols&
 // the value checks of its fixed leaves (Range, Prefix / Suffix of fixed
 // strings) against the staged row; a row failing either takes the exact
 // per-blob path (decode_blob, which reports it), after the column stores.
-template <bool EXT, int NCT>
+template <bool EXT, int NCT, bool VAL = false>
 __device__ __forceinline__ void dfix_status(const DecFixProgram& F, const DecProgram& P, const DecCols& cols,
                                             const uint8_t* lds_raw, const uint32_t* chk, const uint8_t* arena,
                                             const uint64_t* offs, uint32_t* status, uint64_t blob0, uint32_t rows,
@@ -1554,13 +1554,16 @@ __device__ __forceinline__ void dfix_status(const DecFixProgram& F, const DecPro
         const uint64_t i = blob0 + j;
         uint32_t sv = 0;
         if (bad)
-            sv = decode_blob<GReader, EXT>(P, cols, GReader{arena}, offs ? offs[i] : i * B,
-                                           offs ? offs[i + 1] : (i + 1) * B, i);
+            sv = decode_blob<GReader, EXT, VAL>(P, cols, GReader{arena}, offs ? offs[i] : i * B,
+                                                offs ? offs[i + 1] : (i + 1) * B, i);
         status[i] = sv;
     }
 }
 
-template <bool EXT>
+// VAL: ValidateBuffer over the staged tile — the row checks and status only
+// (a row the canonical checks accept is one DecodeBuffer, hence
+// ValidateBuffer, accepts; the others run decode_blob<VAL>)
+template <bool EXT, bool VAL = false>
 __device__ __forceinline__ void dfix_oneshot(const DecFixProgram& F, const DecProgram& P, const DecCols& cols,
                                              const DecColsK& K, const uint8_t* __restrict__ arena,
                                              const uint64_t* __restrict__ offs, uint64_t n,
@@ -1624,14 +1627,16 @@ __device__ __forceinline__ void dfix_oneshot(const DecFixProgram& F, const DecPr
     if (!__syncthreads_and(ok)) {
         for (uint32_t j = tid; j < rows; j += kBlock) {
             const uint64_t i = blob0 + j;
-            status[i] = decode_blob<GReader, EXT>(P, cols, GReader{arena}, offs ? offs[i] : i * B,
-                                                  offs ? offs[i + 1] : (i + 1) * B, i);
+            status[i] = decode_blob<GReader, EXT, VAL>(P, cols, GReader{arena}, offs ? offs[i] : i * B,
+                                                       offs ? offs[i + 1] : (i + 1) * B, i);
         }
         return;
     }
-    dfix_tile<kBlock>(F, cols, K, lds_raw, blob0, rows, (uint32_t)tid);
-    __syncthreads();
-    dfix_status<EXT, kBlock>(F, P, cols, lds_raw, chk, arena, offs, status, blob0, rows, (uint32_t)tid);
+    if (!VAL) {
+        dfix_tile<kBlock>(F, cols, K, lds_raw, blob0, rows, (uint32_t)tid);
+        __syncthreads();
+    }
+    dfix_status<EXT, kBlock, VAL>(F, P, cols, lds_raw, chk, arena, offs, status, blob0, rows, (uint32_t)tid);
 }
 
 template <bool EXT>
@@ -1650,6 +1655,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     DecFixProgram F, DecProgram P, DecCols cols, DecColsK K, const uint8_t* __restrict__ arena,
     const uint64_t* __restrict__ offs, uint64_t n, uint32_t* __restrict__ status, uint64_t tile0) {
     dfix_oneshot<EXT>(F, P, cols, K, arena, offs, n, status, tile0);
+}
+
+// ValidateBuffer of fixed-layout batches whose checks read most of the blob
+template <bool EXT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_validate_fixed(
+    DecFixProgram F, DecProgram P, DecCols cols, DecColsK K, const uint8_t* __restrict__ arena,
+    const uint64_t* __restrict__ offs, uint64_t n, uint32_t* __restrict__ status, uint64_t tile0) {
+    dfix_oneshot<EXT, true>(F, P, cols, K, arena, offs, n, status, tile0);
 }
 
 // =========================================================================
@@ -2773,6 +2786,25 @@ int packos_validate_batch(const packos_schema* cs, const uint8_t* arena, const u
     if (maxd >= kDecDepth) { set_error("schema nesting too deep for the decoder"); return PACKOS_E_UNSUPPORTED; }
     DecCols dc;
     memset(&dc, 0, sizeof(dc));
+    hipStream_t st = (hipStream_t)stream;
+    // fixed layouts whose checks read most of each blob (or blobs of <= 2
+    // lines): the staged-tile path of the fixed decoder, status only
+    const int64_t B = s->all_present_size;
+    if (s->dec_fast == 1 && ((uintptr_t)arena & 15) == 0 && (offsets || stride == (uint64_t)B) &&
+        !s->tune.decode_generic && (s->val_win == 0 || 2 * s->val_win >= B || B <= 128)) {
+        DecFixProgram F = t->dfix;
+        const int64_t tb = B >= 128 ? kDecTileBytesLarge : kDecTileBytes;
+        F.T = (int32_t)std::min<int64_t>(1024, std::max<int64_t>(16, (tb / B) / 16 * 16));
+        const uint32_t T = (uint32_t)F.T, QW = (uint32_t)((B + 3) / 4);
+        const size_t lds = (size_t)T * B + 16 + 12 * QW;
+        DecColsK K;
+        memset(&K, 0, sizeof(K));
+        hipLaunchKernelGGL(s->ext ? k_validate_fixed<true> : k_validate_fixed<false>,
+                           dim3((unsigned)((n + T - 1) / T)), dim3(kBlock), lds, st, F, t->dec, dc, K, arena, offsets,
+                           (uint64_t)n, status, (uint64_t)0);
+        HIP_TRY(hipGetLastError());
+        return PACKOS_OK;
+    }
     DecProgram P = t->dec;
     P.win = (int32_t)s->val_win;
     const size_t ptab = ((s->dnodes.size() * sizeof(DecNode) + 15) & ~(size_t)15) +
@@ -2794,7 +2826,6 @@ int packos_validate_batch(const packos_schema* cs, const uint8_t* arena, const u
         }
         FA.F = ok ? (int32_t)root.kids.size() : 0;
     }
-    hipStream_t st = (hipStream_t)stream;
 #define PACKOS_VALWIN(WC, X) \
     hipLaunchKernelGGL((k_decode_win<WC, X, true>), g, dim3(kBlock), ptab, st, P, dc, FA, arena, offsets, stride, \
                        (uint64_t)n, status)
