@@ -23,7 +23,7 @@ import shutil
 import statistics
 import sys
 
-KSUB = {"decode": ("k_decode",), "get": ("k_get_field",), "encode": ("k_encode",)}
+KSUB = {"decode": ("k_decode",), "validate": ("k_decode", "k_validate"), "get": ("k_get_field",), "encode": ("k_encode",)}
 
 
 def last_json(path):
