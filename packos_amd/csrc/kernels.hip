@@ -2590,10 +2590,11 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
         for (uint64_t x = 0; x < ntiles; x++)
             for (int q = 0; q < 8; q++) h[q] += hp[x * 8 + q];
         fprintf(stderr, "k_encode_tiles lds=%u tiles=%llu clocks/tile: load=%.0f [round2=%.0f blobs=%.0f scan=%.0f] "
-                "frame=%.0f [chunks1=%.0f chunks2=%.0f]\n",
+                "frame=%.0f [chunks1=%.0f chunks2=%.0f] closed-form frame of waves 0..3: %.0f %.0f %.0f %.0f\n",
                 V.lds_total, (unsigned long long)ntiles, (double)h[0] / ntiles, (double)h[4] / ntiles,
                 (double)h[5] / ntiles, (double)h[1] / ntiles, (double)h[2] / ntiles, (double)h[6] / ntiles,
-                (double)h[3] / ntiles);
+                (double)h[3] / ntiles, (double)h[4] / ntiles, (double)h[5] / ntiles, (double)h[6] / ntiles,
+                (double)h[7] / ntiles);
 #endif
         return PACKOS_OK;
     }

@@ -17,7 +17,7 @@ for spec in ${SPECS:-C3:decode C5:decode}; do
       HE="${ALLENV:-}"; [ $v = head ] && HE="$HE ${HEADENV:-}"
       env $HE PACKOS_LIB=$L timeout -k 10 300 python bench.py --config $c --op $op --steps ${STEPS:-20} --no-cpu --no-host --no-warm > gpurun_out/ab_${c}_${op}_$v.log 2>&1
       rc=$?; [ $rc -eq 0 ] || { echo "$c $op $v rc=$rc"; tail -3 gpurun_out/ab_${c}_${op}_$v.log; exit $rc; }
-      python3 -c "import json,sys; l=json.loads([x for x in open(sys.argv[1]) if x.startswith('{')][-1]); print(sys.argv[2], sys.argv[3], sys.argv[4], l['kernel_ms'], l['roofline']['frac'], l['roofline'].get('frac_granularity'))" gpurun_out/ab_${c}_${op}_$v.log $c $op $v | tee -a gpurun_out/ab.jsonl
+      python3 -c "import json,sys; l=json.loads([x for x in open(sys.argv[1]) if x.startswith('{')][-1]); print(sys.argv[2], sys.argv[3], sys.argv[4], l['kernel_ms'], l['roofline']['frac'], l['roofline'].get('frac_granularity'), l.get('parity'))" gpurun_out/ab_${c}_${op}_$v.log $c $op $v | tee -a gpurun_out/ab.jsonl
     done
   done
 done
