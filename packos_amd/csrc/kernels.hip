@@ -2544,8 +2544,26 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
     // (and writes) the out offsets itself, no size pass; otherwise the size pass
     // (or the caller's PACKOS_ENC_OFFSETS_READY offsets) first, loaded per tile.
     VPlan V;
-    const bool affine = !offs_ready && affine_layout(s, ec, nullptr);
-    if (!(flags & PACKOS_ENC_FORCE_GENERIC) && var_plan(s, ec, !affine, V)) {
+    AffPlan A6;
+    const bool affine = !offs_ready && affine_layout(s, ec, &A6);
+    const bool planned = !(flags & PACKOS_ENC_FORCE_GENERIC) && var_plan(s, ec, !affine, V, (uint32_t)s->tune.var_per);
+    // six workgroups per CU (k_encode_tiles<true, NV, 6>) when a closed-form plan with <= 2
+    // var columns fits kVLds6; a batch whose mean var bytes per blob are known
+    // (exact capacity) and <= 28 may shrink its staging pool to 32 B per blob
+    bool six = false;
+    if (planned && V.aff && V.nvar <= 2) {
+        six = V.lds_total <= kVLds6;
+        const uint64_t stat = (uint64_t)A6.C * n;
+        if (!six && (flags & PACKOS_ENC_CAP_EXACT) && n && cap >= stat && (cap - stat) / n <= 28 &&
+            s->tune.var_per > 32) {
+            VPlan V32;
+            if (var_plan(s, ec, !affine, V32, 32u) && V32.aff && V32.lds_total <= kVLds6) {
+                V = V32;
+                six = true;
+            }
+        }
+    }
+    if (planned) {
         if (!affine && !offs_ready) {
             if ((r = size_pass(s, t, ec, n, out_offsets, ws, ws_bytes, st))) return r;
         }
@@ -2564,11 +2582,18 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
 #endif
         // instantiated per var-slot bound: the per-blob loops over var slots
         // (positions, lengths, header offsets) stop at the schema's count
-#define PACKOS_TILES(AFF, NV)                                                                          \
-    hipLaunchKernelGGL((k_encode_tiles<AFF, NV>), dim3((unsigned)ntiles), dim3(kVNT), V.lds_total, st, V, \
+#define PACKOS_TILES(AFF, NV)                                                                             \
+    hipLaunchKernelGGL((k_encode_tiles<AFF, NV, 1>), dim3((unsigned)ntiles), dim3(kVNT), V.lds_total, st, V, \
+                       out_offsets, out, cap, (uint64_t)n, status)
+#define PACKOS_TILES6(NV)                                                                                  \
+    hipLaunchKernelGGL((k_encode_tiles<true, NV, 6>), dim3((unsigned)ntiles), dim3(kVNT), V.lds_total, st, V, \
                        out_offsets, out, cap, (uint64_t)n, status)
         const int nv = V.nvar <= 1 ? 1 : V.nvar <= 2 ? 2 : V.nvar <= 4 ? 4 : 8;
-        if (V.aff) {
+        if (six) {
+            g_last_encoder = "tiles6";
+            if (nv == 1) PACKOS_TILES6(1);
+            else PACKOS_TILES6(2);
+        } else if (V.aff) {
             if (nv == 1) PACKOS_TILES(true, 1);
             else if (nv == 2) PACKOS_TILES(true, 2);
             else if (nv == 4) PACKOS_TILES(true, 4);
@@ -2580,6 +2605,7 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
             else PACKOS_TILES(false, 8);
         }
 #undef PACKOS_TILES
+#undef PACKOS_TILES6
         HIP_TRY(hipGetLastError());
 #ifdef PACKOS_PHASE_PROF
         std::vector<unsigned long long> hp(ntiles * 8);

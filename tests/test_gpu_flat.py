@@ -128,7 +128,7 @@ def test_flat_wide_fixed_leaf_falls_back():
     encoder takes the chain, bit-exact."""
     chain = SChain(SInt64, SVariableString(), SStringLen(40), SBytes(17))
     hc = HostColumns.from_rows(chain, rows(chain, 700, 3))
-    check(chain, hc, 0, "wide fixed", kernel="tiles")
+    check(chain, hc, 0, "wide fixed", kernel=("tiles", "tiles6"))
 
 
 @pytest.mark.parametrize("lens", [[0], [0, 1], [16], [4000, 0], [7000, 9000]], ids=str)
@@ -150,7 +150,8 @@ def test_flat_configs(name, n, flat, monkeypatch, flat_on):
     cfg = CONFIGS[name]
     hc = make_columns(cfg, n=n)
     for mode in (0, 1):
-        check(cfg.chain, hc, mode, f"{name} flat={flat} mode {mode}", kernel=flat_on if flat == "1" else "tiles")
+        check(cfg.chain, hc, mode, f"{name} flat={flat} mode {mode}",
+              kernel=flat_on if flat == "1" else ("tiles", "tiles6"))
 
 
 def test_flat_capacity_overrun():
@@ -180,7 +181,10 @@ def test_flat_capacity_overrun():
 
 @pytest.mark.parametrize("name,cap_scale,flags,want", [
     ("C5", 1, 0, "flat"), ("C5", 3, 0, "flat"), ("C5", 1, 4, "flat"),
-    ("C3", 1, 0, "tiles"), ("C3", 4, 0, "tiles"), ("C3", 1, 4, "tiles"),
+    ("C3", 1, 0, "tiles"), ("C3", 4, 0, "tiles"),
+    # C3 declared exact: 24 var bytes per blob, a 32-B staging pool, six
+    # workgroups per CU (k_encode_tiles<true, 1, 6>)
+    ("C3", 1, 4, "tiles6"),
     # C3 with a capacity of 4x its size, declared exact: the caller's word is taken
     ("C3", 4, 4, "flat")])
 def test_flat_auto_dispatch(name, cap_scale, flags, want, monkeypatch):
