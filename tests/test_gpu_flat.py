@@ -195,3 +195,22 @@ def test_flat_auto_dispatch(name, cap_scale, flags, want, monkeypatch):
     cfg = CONFIGS[name]
     hc = make_columns(cfg, n=3000)
     check(cfg.chain, hc, 0, f"{name} x{cap_scale} flags {flags}", kernel=want, cap_scale=cap_scale, flags=flags)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("n", [1000, 3000 + 77])
+def test_tiles6_pool_overflow_and_tail(mode, n, monkeypatch):
+    """The six-workgroup tile encoder (exact capacity, <= 28 var bytes per
+    blob on average: a 32-B staging pool) on tiles whose var bytes overflow
+    the pool (their values become holes, the kernel's spilled path), mixed
+    with staged tiles and a ragged last tile; bit-exact against the oracle."""
+    monkeypatch.delenv("PACKOS_ENC_FLAT", raising=False)
+    chain = SChain(SInt32, SVariableString(), SInt64, SStringLen(8))
+    rng = random.Random(n + mode)
+    rws = []
+    for i in range(n):
+        t = i // 128
+        ln = rng.randint(0, 120) if t % 5 == 2 else rng.randint(0, 24)   # every 5th tile overflows
+        rws.append([i - 500, "x" * ln, (i * 7919) - 10 ** 12, "abcdefgh"])
+    hc = HostColumns.from_rows(chain, rws)
+    check(chain, hc, mode, f"tiles6 n={n} mode {mode}", kernel="tiles6", flags=_lib.ENC_CAP_EXACT)
