@@ -505,7 +505,8 @@ const char* packos_last_error(void);   /* thread-local detail of the last failur
 int         packos_abi_version(void);
 /* Diagnostics: the encode kernel the last packos_encode_batch call of this
  * thread launched ("fixed_tile", "fixed_dw", "fixed", "var", "ext", "flat",
- * "tiles"; "" before any call and after a call that launched none).  No reference counterpart; tests use it to
+ * "tiles", "tiles6" = the tile encoder at six workgroups per CU; "" before
+ * any call and after a call that launched none).  No reference counterpart; tests use it to
  * assert which encoder a batch exercised.                                      */
 const char* packos_last_encoder(void);
 
