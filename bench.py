@@ -358,13 +358,15 @@ def get_parity(arena, offsets, stride, n, path, getter, gvals, gst):
     return same, int(ok.sum()), hashlib.sha256(g_vals.tobytes() + g_st.tobytes()).hexdigest()[:16]
 
 
-def pcie_ceiling(dev, nbytes=256 << 20, repeats=3, pieces=(4 << 20, 16 << 20, 64 << 20)):
+def pcie_ceiling(dev, nbytes=1 << 30, repeats=3, pieces=(4 << 20, 16 << 20, 64 << 20, 256 << 20)):
     """Pinned host <-> device copy rates of this box (GB/s) with plain HIP
     calls (libamdhip64 through ctypes): H2D alone, D2H alone, and both at once
     on two streams, each the BEST over `repeats` runs at every copy size in
     `pieces` (the host pipeline moves 4-64 MiB chunks, three in flight), so the
-    ceiling is the link's, not one copy shape's.  `bidir_total_gbs` = both
-    directions' bytes / time."""
+    ceiling is the link's, not one copy shape's.  1 GiB per run: with 256 MiB
+    runs the per-copy launch overhead held the probe ~1 % under what the C5
+    host pipeline then reached (frac_of_pcie 1.006).  `bidir_total_gbs` =
+    both directions' bytes / time."""
     import ctypes as C
     import torch
     torch.cuda.synchronize()
