@@ -7,6 +7,12 @@ One step = one encode of this GPU's whole shard with its inputs already
 resident in HBM (metric config M: 1M x 256 B fixed-schema tuples per GPU;
 C5: one 8,388,608-blob shard of the 64M mixed batch).
 
+Ranks: `--gpus N` (N > 1) with no launcher around it starts N rank processes
+itself (a child `torch.distributed.run --nproc-per-node N` on this script,
+before any GPU call; the parent waits and exits with the job's status); under
+an external launcher every rank checks WORLD_SIZE == N and, under nccl
+(RCCL), a distinct GPU per rank, and exits non-zero otherwise.
+
 Batch and shards: the N ranks encode N disjoint contiguous shards of ONE
 global synthetic batch of N x (blobs per GPU) blobs (weak scaling), planned
 byte-balanced by packos_amd.shard.plan_shards; each rank generates exactly
@@ -505,20 +511,69 @@ def host_leg(schema, hc, dev):
     return enc
 
 
+# ----------------------------------------------------------------- ranks
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_cmd(gpus, env, argv, port=None):
+    """The command that starts `gpus` rank processes of this bench, or None
+    when this process is itself a rank (gpus == 1, or a launcher already set
+    WORLD_SIZE).  `python bench.py --gpus N` with no launcher around it runs
+    `torch.distributed.run --nproc-per-node N` on itself as a child, before
+    anything here touches the GPU; the parent only waits for it."""
+    if gpus <= 1 or "WORLD_SIZE" in env or env.get("PACKOS_BENCH_RANK_CHILD"):
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(port or _free_port()),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def world_error(gpus, world, backend, device_count, local_world, local):
+    """Why this rank must not run (a message), or None: the job must have
+    exactly --gpus ranks, and under nccl (RCCL) every local rank needs a
+    device of its own."""
+    if world != gpus:
+        return f"bench.py: --gpus {gpus} but the job has {world} rank(s) (WORLD_SIZE); refusing to label the run"
+    if backend == "nccl" and world > 1:
+        if device_count < local_world:
+            return (f"bench.py: {local_world} ranks on this node but torch.cuda.device_count() = {device_count}: "
+                    f"--gpus {gpus} needs a GPU per rank")
+        if not 0 <= local < device_count:
+            return f"bench.py: local rank {local} has no device (device_count {device_count})"
+    return None
+
+
 # ----------------------------------------------------------------- main
 def main():
     args = parse()
+    cmd = launch_cmd(args.gpus, os.environ, sys.argv[1:])
+    if cmd is not None:
+        # parent of N ranks: no GPU work here; exit with the job's status
+        import subprocess
+        env = dict(os.environ, PACKOS_BENCH_RANK_CHILD="1")
+        sys.exit(subprocess.run(cmd, env=env, cwd=ROOT).returncode)
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     # rehearsal knobs (tests only): every rank on one device, gloo for the
     # harness barrier / timing all-reduce; the driver's runs use neither
     if os.environ.get("PACKOS_BENCH_DEVICE") is not None:
         local = int(os.environ["PACKOS_BENCH_DEVICE"])
     backend = os.environ.get("PACKOS_BENCH_BACKEND", "nccl")
+    err = world_error(args.gpus, world, backend, torch.cuda.device_count(), local_world, local)
+    if err:
+        print(err, file=sys.stderr, flush=True)
+        sys.exit(3)
     if world > 1:
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -528,6 +583,17 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    # rank -> device map (PCI bus of each rank's GPU), reported in `config`
+    props = torch.cuda.get_device_properties(dev)
+    me = {"rank": rank, "device": dev.index, "pci_bus": getattr(props, "pci_bus_id", None),
+          "host": platform.node()}
+    rank_map = [me]
+    if world > 1:
+        rank_map = [None] * world
+        dist.all_gather_object(rank_map, me)
+        if backend == "nccl" and len({(m["host"], m["device"]) for m in rank_map}) != world:
+            print(f"bench.py: ranks share a device under nccl: {rank_map}", file=sys.stderr, flush=True)
+            sys.exit(3)
 
     from packos_amd.api import CompiledSchema, DeviceColumns, EncodePlan
     from packos_amd.configs import CONFIGS, algorithmic_bytes, make_columns
@@ -815,6 +881,8 @@ def main():
             "config": {"workload": f"{args.config}: {cfg.note}", "op": args.op, "blobs_per_gpu": n, "global_blobs": n_global,
                        "blob_bytes": schema.fixed_blob_size if fixed else round(total_out / n, 1),
                        "parallelism": f"dp{world} (byte-balanced disjoint shards, no collective)",
+                       "backend": backend if world > 1 else None, "world_size": world,
+                       "rank_devices": [[m["rank"], m["device"], m["pci_bus"]] for m in rank_map],
                        "sets_rotated": len(sets), "footprint_mib": round(footprint / 2 ** 20, 1),
                        **({"get": f"GetInt(pos {args.get_pos}) -> " + ("value, start, len, tag, status" if args.get_spans
                                                                        else "value, status")}

@@ -293,10 +293,18 @@ int packos_encoded_size_batch(const packos_schema* s, const packos_column* cols,
  * packos_encoded_size_batch): the library takes out_capacity / n as the mean
  * blob size when it picks the kernel for a flat chain of leaves with every
  * value present.  Without it, a batch whose capacity admits >= 256 bytes per
- * blob has its var columns' first and last offsets read back (a small copy
- * on `stream` and a wait for it) to compute that mean.  Results never depend
- * on the choice.                                                             */
+ * blob launches both candidate kernels and each decides on the device from
+ * the var columns' first and last offsets (no host read-back: every call
+ * stays asynchronous on `stream` and can be captured in a HIP graph).
+ * Results never depend on the choice.                                        */
 #define PACKOS_ENC_CAP_EXACT 4u
+/* out_offsets (n+1, device) already hold packos_encoded_size_batch's result
+ * for these same columns: the library does not run the size pass again.  A
+ * closed-form layout (no presence depending on the data) is recomputed by the
+ * encoder itself (the same offsets, rewritten), so its fast kernels stay
+ * eligible; other layouts are encoded into the given offsets as with
+ * PACKOS_ENC_OFFSETS_READY.                                                  */
+#define PACKOS_ENC_SIZED 8u
 /* testing/benchmark knob: pick the fixed-layout kernel variant (0 = auto):
  * 13 one tile per workgroup, LDS-DMA staging, single-source dwords (auto
  *    when B % 4 == 0, 16 <= B <= 1024, <= 16 fixed columns);

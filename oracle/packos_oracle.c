@@ -135,6 +135,12 @@ int or_schema_prepare(or_schema* s) {
     s->n_cols = col;
     return 0;
 }
+/* top-level fields an encode writes: EncodeValueNamed walks FieldNames
+ * (schema.go:976), so a SchemaNamedChain with fewer names than schemas
+ * writes only the first len(FieldNames) of them                              */
+static int enc_top(const or_schema* s) {
+    return s->chain_names > 0 && s->chain_names < s->n_top ? s->chain_names : s->n_top;
+}
 
 static int leaf_tag(int k) {
     switch (k) {
@@ -377,8 +383,8 @@ static int x_field(const or_schema* s, const packos_column* cols, size_t i, int 
 static int64_t x_encode(const or_schema* s, const packos_column* cols, size_t i, int mode, xbuf* b) {
     b->len = 0;
     int64_t slack = 0;
-    if (mode == PACKOS_MODE_PACKABLE && s->n_top == 0) return 0;   /* Pack() with no args */
-    x_container(s, cols, i, s->top_nodes, s->n_top, PACKOS_TAG_TUPLE, mode, b, &slack);
+    if (mode == PACKOS_MODE_PACKABLE && enc_top(s) == 0) return 0;   /* Pack() with no args */
+    x_container(s, cols, i, s->top_nodes, enc_top(s), PACKOS_TAG_TUPLE, mode, b, &slack);
     if (mode == PACKOS_MODE_PACKABLE && slack) {
         grow(&b->p, &b->cap, b->len + (size_t)slack + 1);
         memset(b->p + b->len, 0, (size_t)slack);
@@ -394,16 +400,17 @@ int64_t or_encoded_size_one(const or_schema* s, const packos_column* cols, size_
         free(b.p);
         return r;
     }
+    const int nt = enc_top(s);
     if (mode == PACKOS_MODE_PACKABLE) {
-        if (s->n_top == 0) return 0;
+        if (nt == 0) return 0;
         int64_t sz = 0;
-        for (int t = 0; t < s->n_top; t++) sz += pk_value_size(s, cols, i, s->top_nodes[t]);
-        return sz + 2 * (int64_t)s->n_top + 2;
+        for (int t = 0; t < nt; t++) sz += pk_value_size(s, cols, i, s->top_nodes[t]);
+        return sz + 2 * (int64_t)nt + 2;
     }
     or_put p, pool[16];
     or_put_init(&p);
     for (int d = 0; d < 16; d++) or_put_init(&pool[d]);
-    for (int t = 0; t < s->n_top; t++) put_node(s, cols, i, s->top_nodes[t], &p, pool, 0);
+    for (int t = 0; t < nt; t++) put_node(s, cols, i, s->top_nodes[t], &p, pool, 0);
     int64_t sz = (int64_t)or_put_pack_size(&p);
     or_put_free(&p);
     for (int d = 0; d < 16; d++) or_put_free(&pool[d]);
@@ -469,16 +476,17 @@ static int64_t encode_one_tls(const or_schema* s, const packos_column* cols, siz
         free(b.p);
         return r;
     }
+    const int nt = enc_top(s);
     if (mode == PACKOS_MODE_PACKABLE) {
         /* packable.Pack: buffer of ValueSize() bytes, zero filled (pack.go:59-67) */
-        if (s->n_top == 0) return 0;
+        if (nt == 0) return 0;
         int64_t size = 0;
-        for (int k = 0; k < s->n_top; k++) size += pk_value_size(s, cols, i, s->top_nodes[k]);
-        size += 2 * (int64_t)s->n_top + 2;
-        if ((size_t)size > cap) return -1;
+        for (int k = 0; k < nt; k++) size += pk_value_size(s, cols, i, s->top_nodes[k]);
+        size += 2 * (int64_t)nt + 2;
+        if (size < 0 || (size_t)size > cap) return -1;
         memset(out, 0, (size_t)size);
-        int64_t hsz = 2 * (int64_t)s->n_top + 2, posH = 0, pos = hsz, delta = hsz;
-        for (int k = 0; k < s->n_top; k++) {
+        int64_t hsz = 2 * (int64_t)nt + 2, posH = 0, pos = hsz, delta = hsz;
+        for (int k = 0; k < nt; k++) {
             int n = s->top_nodes[k];
             int64_t off = k == 0 ? hsz : pos - delta;
             if (ovf(off)) *overflow = 1;
@@ -491,7 +499,7 @@ static int64_t encode_one_tls(const or_schema* s, const packos_column* cols, siz
         return size;
     }
     or_put_reset(&t->p);
-    for (int k = 0; k < s->n_top; k++) put_node(s, cols, i, s->top_nodes[k], &t->p, t->pool, 0);
+    for (int k = 0; k < nt; k++) put_node(s, cols, i, s->top_nodes[k], &t->p, t->pool, 0);
     size_t need = or_put_pack_size(&t->p);
     if (need > cap) return -1;
     size_t got = or_put_pack(&t->p, out);
@@ -529,15 +537,22 @@ static void* enc_worker(void* arg) {
         encode_one_tls(j->s, j->cols, i, j->mode, j->out + j->offs[i], cap, &o, &t);
         if (j->status) {
             uint32_t sv = o ? PACKOS_STATUS_OVERFLOW13 : 0u;
-            const int chk = j->s->ext != NULL || has_names_bad(j->s);
-            for (int tp = 0; chk && tp < j->s->n_top; tp++) {
+            const int more_names = j->s->chain_names > j->s->n_top;
+            const int chk = j->s->ext != NULL || has_names_bad(j->s) || more_names;
+            int failed = 0;
+            for (int tp = 0; chk && tp < enc_top(j->s); tp++) {
                 int inner = enc_check(j->s, j->cols, i, j->s->top_nodes[tp]);
                 if (inner) {
                     /* SchemaError(ErrEncode, ChainName, "", -1, err): position -1 (schema.go:919-936) */
                     sv |= (uint32_t)PACKOS_ERR_ENCODE | ((uint32_t)inner << 24);
+                    failed = 1;
                     break;
                 }
             }
+            /* EncodeValueNamed with more FieldNames than Schemas: every schema's
+             * field written, the next name indexes chain.Schemas[len(Schemas)]
+             * (schema.go:976-987) -- a Go runtime panic, no bytes              */
+            if (more_names && !failed) sv = PACKOS_STATUS_PANIC;
             j->status[i] = sv;
         }
     }
@@ -845,6 +860,10 @@ static uint32_t decode_one(const or_schema* s, const uint8_t* blob, int64_t len,
     } else if (or_seq_init(&q, blob, len)) {
         return (uint32_t)PACKOS_ERR_INVALID_FORMAT; /* pos -1 */
     }
+    /* DecodeBufferNamed (schema.go:948-956): NewSeqGetAccess first, then the
+     * length check fails every blob -- ErrConstraintViolated, position -1.
+     * ValidateBuffer takes the plain SchemaChain (val): no such check.       */
+    if (s->chain_names && !val) return (uint32_t)PACKOS_ERR_CONSTRAINT_VIOLATED;
     dec_ctx c = {s, cols, i, base, ext, val};
     for (int t = 0; t < s->n_top; t++) {
         int e = dec_node(&c, s->top_nodes[t], &q, base);

@@ -87,6 +87,15 @@ typedef struct or_schema {
      *   [1] min  [2] max
      *   [3] (prefix/suffix literal index + 1) | (default literal index + 1) << 32 */
     const int64_t* ext;
+    /* SchemaNamedChain (schema.go:943-946) whose len(FieldNames) differs from
+     * len(Schemas): that FieldNames length, else 0.  EncodeValueNamed walks
+     * FieldNames (schema.go:968-995): with fewer names only the first
+     * chain_names schemas are encoded; with more, the walk indexes past
+     * Schemas once the present fields are written (a Go panic).
+     * DecodeBufferNamed fails every blob NewSeqGetAccess accepts
+     * (schema.go:953-956).  ValidateBuffer takes the plain SchemaChain: no
+     * change.                                                                */
+    int            chain_names;
 } or_schema;
 
 int or_schema_prepare(or_schema* s);   /* 0 ok */

@@ -18,7 +18,8 @@ MODE_PACKABLE = 1
 MODE_EXTENDED = 0x100   # ADR-001 extended containers (include/packos.h), OR-ed into a mode
 ENC_OFFSETS_READY = 1
 ENC_FORCE_GENERIC = 2
-ENC_CAP_EXACT = 4       # out_capacity is the batch's exact encoded size (kernel choice without a read-back)
+ENC_CAP_EXACT = 4       # out_capacity is the batch's exact encoded size (the kernel choice is made on the host)
+ENC_SIZED = 8           # out_offsets hold packos_encoded_size_batch's result (no second size pass)
 
 
 def ENC_FIXED_VARIANT(v: int) -> int:

@@ -223,11 +223,11 @@ def encode_batch(schema: CompiledSchema, cols: DeviceColumns, want_offsets: bool
     total = int(offs[n].item()) if n else 0
     if out is None or out.numel() < total:
         out = torch.empty(max(total, 16), dtype=torch.uint8, device=dev)
-    if cols.any_valid():
-        flags |= _lib.ENC_OFFSETS_READY   # presence depends on the data: keep the size pass's layout
-    elif out.numel() == total:
-        flags |= _lib.ENC_CAP_EXACT       # closed form: the encoder writes the same offsets itself
-    check(L.packos_encode_batch(schema.handle, arr, n, out.data_ptr(), out.numel(), offs.data_ptr(),
+    # the size pass above gave the layout and the exact size: no second size
+    # pass (a closed-form layout is rewritten identically by the encoder), and
+    # the kernel choice from the exact size (no read-back, no device pick)
+    flags |= _lib.ENC_SIZED | _lib.ENC_CAP_EXACT
+    check(L.packos_encode_batch(schema.handle, arr, n, out.data_ptr(), total, offs.data_ptr(),
                                 None if status is None else status.data_ptr(), ws.data_ptr(), wsb,
                                 flags, st), "packos_encode_batch")
     return EncodeResult(out, offs, status[:n] if status is not None else None, total, -1)
@@ -425,8 +425,12 @@ class EncodePlan:
         self.out = out if out is not None else torch.empty(max(self.total, 16), dtype=torch.uint8, device=dev)
         if self.out.numel() < self.total:
             raise ValueError("EncodePlan: `out` is smaller than the batch's encoded size")
-        if not self.fixed and self.out.numel() == self.total:
-            self.flags |= _lib.ENC_CAP_EXACT   # the arena is the batch's exact size (from the size pass)
+        # the capacity passed is the batch's exact size (known from the size
+        # pass above, whatever `out` holds beyond it): the kernel choice is made
+        # on the host and run() never reads anything back
+        self.cap = self.out.numel() if self.fixed else self.total
+        if not self.fixed:
+            self.flags |= _lib.ENC_CAP_EXACT
 
     def run(self):
         L = lib()
@@ -439,7 +443,7 @@ class EncodePlan:
             return self.out
         # one call: the size kernel (sizes + look-back scan -> offsets) and the
         # encode kernel; `offsets` is rewritten by every run
-        check(L.packos_encode_batch(self.schema.handle, self._arr, n, self.out.data_ptr(), self.out.numel(),
+        check(L.packos_encode_batch(self.schema.handle, self._arr, n, self.out.data_ptr(), self.cap,
                                     self.offsets.data_ptr(), stp, self.ws.data_ptr(), self.wsb,
                                     self.flags, st), "packos_encode_batch")
         return self.out

@@ -109,13 +109,18 @@ class HostColumns:
         arenas = [bytearray() for _ in range(ncol)]
         offs = [[0] for _ in range(ncol)]
         valid = [[] for _ in range(ncol)]
+        # EncodeValueNamed reads field i under FieldNames[i]: a schema past the
+        # names gets no value and is never encoded (schema.go:976)
+        named = isinstance(chain, SchemaNamedChain) and len(chain.FieldNames) > 0
+        nenc = min(len(chain.FieldNames), len(chain.Schemas)) if named else len(chain.Schemas)
         for row in rows:
             vals = row if isinstance(row, (list, tuple)) else [row]
             if isinstance(chain, SchemaNamedChain) and isinstance(row, dict):
-                vals = [row.get(nm) for nm in chain.FieldNames]
+                vals = [row.get(nm) for nm in chain.FieldNames[:len(chain.Schemas)]]
+            vals = list(vals) + [None] * (len(chain.Schemas) - len(vals))
             col = [0]
-            for node, v in zip(chain.Schemas, vals):
-                hc._put(node, v, col, fixed, arenas, offs, valid, present=True)
+            for j, (node, v) in enumerate(zip(chain.Schemas, vals)):
+                hc._put(node, v, col, fixed, arenas, offs, valid, present=j < nenc)
         for c, sp in enumerate(hc.specs):
             if sp.fixed:
                 hc.data[c] = np.frombuffer(bytes(fixed[c]), dtype=np.uint8).copy()

@@ -483,7 +483,25 @@ struct Builder {
             s->conts[0].hdr_item = 0;
             return;
         }
-        emit_container(0, 0);
+        {
+            // EncodeValueNamed walks FieldNames (schema.go:976): a SchemaNamedChain
+            // with fewer names than schemas writes only the first len(FieldNames)
+            std::vector<int> top = s->nodes[0].kids;
+            if (s->chain_names > 0 && (size_t)s->chain_names < top.size()) s->nodes[0].kids.resize(s->chain_names);
+            emit_container(0, 0);
+            s->nodes[0].kids = top;
+            if (s->chain_names > 0 && (size_t)s->chain_names > top.size()) {
+                // ... and with more names it indexes chain.Schemas[len(Schemas)] once
+                // every schema's field is written (:976-987): a Go panic for every
+                // blob whose fields all encode (k_encode_checks, CHK_PANIC last)
+                EncCheck k{};
+                k.col = -1;
+                k.cont = 0;
+                k.top = -1;
+                k.flags = CHK_PANIC;
+                s->echk.push_back(k);
+            }
+        }
         if (s->items.size() > 65000) fail(PACKOS_E_UNSUPPORTED, "schema too large");
         // per-item kernel aux data: var slot, staging region, divide magic
         int nv = 0, nr = 0;
@@ -546,6 +564,10 @@ struct Builder {
         }
         s->all_present_overflow = ovf;
         if (B <= 0 || B > 1024) return;  // large fixed blobs use the general kernel
+        // a SchemaNamedChain whose names and schemas differ: the tile tables
+        // cover every column, the encode layout only the named fields (rare:
+        // the general kernel takes it)
+        if (s->chain_names) return;
 
         // tile size: T blobs (multiple of 16 so tile in/out are whole 16-B chunks)
         // ~16 KiB of output per tile (env PACKOS_TILE_BYTES overrides, tuning only)
@@ -614,7 +636,7 @@ struct Builder {
         }
         s->dvchk.clear();
         for (const EncCheck& c : s->echk) {
-            if (c.flags & CHK_FAIL) continue;   // no value to check (the decoder fails the blob itself)
+            if (c.flags & (CHK_FAIL | CHK_PANIC)) continue;   // no value to check (the decoder fails the blob itself)
             DecChk v{};
             for (const DecFix& df : s->dfix)
                 if (df.col == c.col) v.blob_off = df.blob_off;
@@ -934,9 +956,10 @@ int packos_schema_compile(const char* schema_json, int mode, packos_schema** out
             // SchemaNamedChain whose FieldNames and Schemas differ in length:
             // DecodeBufferNamed fails every blob, EncodeValueNamed writes only
             // len(FieldNames) fields or indexes past Schemas (schema.go:953-956,
-            // 975-994) — fenced off here
+            // 975-994): build_encode, k_encode_checks (CHK_PANIC) and
+            // packos_decode_batch (k_decode_chain_names) follow chain_names
             if (names && names->kind == JVal::ARR && !names->arr.empty() && names->arr.size() != list->arr.size())
-                fail(PACKOS_E_SCHEMA, "SchemaNamedChain: fieldNames and schema differ in length");
+                s->chain_names = (int)names->arr.size();
         } else if (j.kind == JVal::OBJ) {
             single.kind = JVal::ARR;
             single.arr.push_back(j);
@@ -989,7 +1012,9 @@ int packos_schema_compile(const char* schema_json, int mode, packos_schema** out
         }
         b.build_fixed();
         b.build_decode();
-        s->dec_fast = canonical_decodes(s) ? 1 : 0;
+        // (the fixed-layout decoder follows the ENCODE layout, which a
+        // SchemaNamedChain with fewer names than schemas cuts short)
+        s->dec_fast = !s->chain_names && canonical_decodes(s) ? 1 : 0;
         b.build_info();
         b.build_describe();
     } catch (const CompileError& e) {

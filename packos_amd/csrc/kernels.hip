@@ -567,6 +567,10 @@ __global__ __launch_bounds__(kBlock) void k_encode_checks(const EncCheck* __rest
     const uint64_t pm = need_pm ? present_mask(P, cols, i) : ~0ull;
     for (int k = 0; k < nchk; k++) {
         const EncCheck c = chk[k];
+        if (c.flags & CHK_PANIC) {   // every field written, then the Go index panic (no bytes)
+            status[i] = PACKOS_STATUS_PANIC;
+            return;
+        }
         if (!((pm >> c.cont) & 1ull)) continue;
         bool bad;
         if (c.flags & CHK_FAIL) {
@@ -2228,6 +2232,27 @@ int launch_add_base(uint64_t* offs, size_t n, uint64_t add, hipStream_t st) {
 }
 }  // namespace packos
 
+namespace {
+// DecodeBufferNamed over a SchemaNamedChain whose FieldNames and Schemas differ
+// in length (schema.go:948-956): NewSeqGetAccess, then the length check fails
+// every blob — ErrInvalidFormat or ErrConstraintViolated, both at position -1.
+// Thread per blob; the output columns are not written (DecodeBufferNamed
+// returns nil).
+template <bool EXT>
+__global__ __launch_bounds__(kBlock) void k_decode_chain_names(const uint8_t* __restrict__ arena,
+                                                               const uint64_t* __restrict__ offs, uint64_t stride,
+                                                               uint64_t n, uint32_t* __restrict__ status) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t a0 = offs ? offs[i] : i * stride, a1 = offs ? offs[i + 1] : (i + 1) * stride;
+    const GReader R{arena};
+    const int xroot = EXT && a1 - a0 >= 2 && rd16r(R, a0) == kExtMarker ? PACKOS_TAG_TUPLE : 0;
+    DSeq q;
+    status[i] = dseq_init(q, R, a0, (int64_t)(a1 - a0), xroot) ? (uint32_t)PACKOS_ERR_INVALID_FORMAT
+                                                                : (uint32_t)PACKOS_ERR_CONSTRAINT_VIOLATED;
+}
+}  // namespace
+
 extern "C" {
 
 void packos_schema_free(packos_schema* s) {
@@ -2341,31 +2366,6 @@ int packos_encoded_size_batch(const packos_schema* cs, const packos_column* cols
 }
 
 static thread_local const char* g_last_encoder = "";   // packos_last_encoder
-
-// Mean encoded blob size of a closed-form batch: n * C static bytes plus the
-// var columns' byte ranges (off[n] - off[0]).  PACKOS_ENC_CAP_EXACT: the
-// caller's out_capacity is the batch's exact size; otherwise the 2 offsets per
-// var column are read back (a 16-B-per-column copy on the call's stream and a
-// wait for it: only for batches whose capacity admits >= kFlatMinBlob per blob).
-static int mean_blob_bytes(const AffPlan& A, size_t n, uint64_t cap, uint32_t flags, hipStream_t st, uint64_t* mean) {
-    if ((flags & PACKOS_ENC_CAP_EXACT) || A.nv == 0) {
-        *mean = (A.nv == 0 ? A.C * n : cap) / n;
-        return PACKOS_OK;
-    }
-    static thread_local uint64_t* pin = nullptr;   // 2 words per var column, pinned once per thread
-    if (!pin) HIP_TRY(hipHostMalloc((void**)&pin, 2 * kAffVar * sizeof(uint64_t), hipHostMallocDefault));
-    for (int v = 0; v < A.nv; v++) {
-        const size_t w = ((A.w8 >> v) & 1u) ? 8 : 4;
-        pin[2 * v] = pin[2 * v + 1] = 0;
-        HIP_TRY(hipMemcpyAsync(&pin[2 * v], A.off[v], w, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipMemcpyAsync(&pin[2 * v + 1], (const uint8_t*)A.off[v] + n * w, w, hipMemcpyDeviceToHost, st));
-    }
-    HIP_TRY(hipStreamSynchronize(st));
-    uint64_t bytes = A.C * n;
-    for (int v = 0; v < A.nv; v++) bytes += pin[2 * v + 1] - pin[2 * v];
-    *mean = bytes / n;
-    return PACKOS_OK;
-}
 
 static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& ec, bool any_nil, size_t n,
                              uint8_t* out, uint64_t cap, uint64_t* out_offsets, uint32_t* status, void* ws,
@@ -2500,7 +2500,7 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
     if (s->ext) {
         // ADR-001 extended containers: size pass (unless given), then one
         // wavefront per blob
-        if (!offs_ready) {
+        if (!offs_ready && !(flags & PACKOS_ENC_SIZED)) {
             if ((r = size_pass(s, t, ec, n, out_offsets, ws, ws_bytes, st))) return r;
         }
         const size_t lds = (size_t)kWavesPerBlock * ext_pos_words((int)s->items.size()) * 4;
@@ -2516,20 +2516,35 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
     // Small blobs stay on k_encode_tiles, whose frame builds the whole output
     // image in LDS (C3, 85-B blobs: 0.060 ms there vs 0.106 ms here); large
     // blobs stream their values straight from HBM here (C5, 969-B blobs: 3.57
-    // ms vs 4.29).  The choice follows the batch's mean blob size: the static
-    // bytes plus the var bytes (mean_blob_bytes).
-    AffPlan A;
-    if (s->tune.enc_flat != 0 && !offs_ready && !(flags & PACKOS_ENC_FORCE_GENERIC) && affine_layout(s, ec, &A)) {
-        bool flat_ok = s->tune.enc_flat == 1;
-        if (!flat_ok && n && cap / n >= kFlatMinBlob) {   // cap / n bounds the mean from above
-            uint64_t mean = 0;
-            if ((r = mean_blob_bytes(A, n, cap, flags, st, &mean))) return r;
-            flat_ok = mean >= kFlatMinBlob;
+    // ms vs 4.29).  The choice follows the batch's mean blob size (static
+    // bytes + var bytes): out_capacity / n when the caller says it is exact
+    // (PACKOS_ENC_CAP_EXACT) or when it is below kFlatMinBlob (an upper bound
+    // of the mean); otherwise BOTH kernels are launched and decide on the
+    // device (pick_skip, encode_var.inc) — nothing is read back, so the call
+    // never waits on the host and can be captured in a graph.
+    const bool sized = (flags & PACKOS_ENC_SIZED) != 0;
+    AffPlan A{};
+    const bool affine = !offs_ready && affine_layout(s, ec, &A);
+    // PACKOS_ENC_SIZED: out_offsets already hold the size pass's layout — used
+    // as given unless the layout is closed form (the encoders rewrite the same
+    // offsets themselves, and the closed-form kernels are the fast ones)
+    const bool use_given = offs_ready || (sized && !affine);
+    VPlan V;
+    const bool planned = !(flags & PACKOS_ENC_FORCE_GENERIC) && var_plan(s, ec, !affine, V, (uint32_t)s->tune.var_per);
+    FPlan F;
+    uint32_t pick = 0;
+    if (s->tune.enc_flat != 0 && affine && !(flags & PACKOS_ENC_FORCE_GENERIC) && flat_plan(s, ec, F)) {
+        bool flat = s->tune.enc_flat == 1;
+        if (!flat && n && cap / n >= kFlatMinBlob) {   // cap / n bounds the mean from above
+            if ((flags & PACKOS_ENC_CAP_EXACT) || A.nv == 0) flat = (A.nv == 0 ? (uint64_t)A.C : cap / n) >= kFlatMinBlob;
+            else if (planned) pick = 1;                 // decided per batch on the device
+            else flat = true;                           // (no tile plan: the flat encoder beats the generic one)
         }
-        FPlan F;
-        if (flat_ok && flat_plan(s, ec, F)) {
+        if (flat || pick) {
+            F.pick = pick;
+            F.pick_C = A.C;
             const dim3 g((unsigned)((n + kFT - 1) / kFT));
-            g_last_encoder = "flat";
+            g_last_encoder = pick ? "flat|tiles" : "flat";
 #define PACKOS_FLAT(NV) \
     hipLaunchKernelGGL((k_encode_flat<NV>), g, dim3(kFNT), F.lds_total, st, F, out_offsets, out, cap, (uint64_t)n, status)
             if (F.nvar <= 1) PACKOS_FLAT(1);
@@ -2537,23 +2552,19 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
             else PACKOS_FLAT(4);
 #undef PACKOS_FLAT
             HIP_TRY(hipGetLastError());
-            return PACKOS_OK;
+            if (!pick) return PACKOS_OK;
         }
     }
     // default: k_encode_tiles.  Data-independent presence: the kernel computes
     // (and writes) the out offsets itself, no size pass; otherwise the size pass
     // (or the caller's PACKOS_ENC_OFFSETS_READY offsets) first, loaded per tile.
-    VPlan V;
-    AffPlan A6;
-    const bool affine = !offs_ready && affine_layout(s, ec, &A6);
-    const bool planned = !(flags & PACKOS_ENC_FORCE_GENERIC) && var_plan(s, ec, !affine, V, (uint32_t)s->tune.var_per);
     // six workgroups per CU (k_encode_tiles<true, NV, 6>) when a closed-form plan with <= 2
     // var columns fits kVLds6; a batch whose mean var bytes per blob are known
     // (exact capacity) and <= 28 may shrink its staging pool to 32 B per blob
     bool six = false;
     if (planned && V.aff && V.nvar <= 2) {
         six = V.lds_total <= kVLds6;
-        const uint64_t stat = (uint64_t)A6.C * n;
+        const uint64_t stat = (uint64_t)A.C * n;
         if (!six && (flags & PACKOS_ENC_CAP_EXACT) && n && cap >= stat && (cap - stat) / n <= 28 &&
             s->tune.var_per > 32) {
             VPlan V32;
@@ -2563,8 +2574,10 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
             }
         }
     }
+    V.pick = pick ? 2u : 0u;
+    V.pick_C = A.C;
     if (planned) {
-        if (!affine && !offs_ready) {
+        if (!affine && !use_given) {
             if ((r = size_pass(s, t, ec, n, out_offsets, ws, ws_bytes, st))) return r;
         }
         V.lits = t->enc.lits;
@@ -2573,7 +2586,7 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
             V.seg[V.oseg].r0 = V.seg[V.oseg].lds + (uint32_t)((uintptr_t)out_offsets & 15);
         }
         const uint64_t ntiles = (n + kVT - 1) / kVT;
-        g_last_encoder = "tiles";
+        g_last_encoder = pick ? "flat|tiles" : "tiles";
 #ifdef PACKOS_PHASE_PROF
         unsigned long long* prof = nullptr;   // debug build only: per-tile phase clocks
         HIP_TRY(hipMalloc(&prof, ntiles * 8 * sizeof(unsigned long long)));
@@ -2590,7 +2603,7 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
                        out_offsets, out, cap, (uint64_t)n, status)
         const int nv = V.nvar <= 1 ? 1 : V.nvar <= 2 ? 2 : V.nvar <= 4 ? 4 : 8;
         if (six) {
-            g_last_encoder = "tiles6";
+            g_last_encoder = pick ? "flat|tiles6" : "tiles6";
             if (nv == 1) PACKOS_TILES6(1);
             else PACKOS_TILES6(2);
         } else if (V.aff) {
@@ -2624,7 +2637,7 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
 #endif
         return PACKOS_OK;
     }
-    if (!offs_ready) {
+    if (!use_given) {
         if ((r = size_pass(s, t, ec, n, out_offsets, ws, ws_bytes, st))) return r;
     }
     const size_t npos = s->items.size() + 1;
@@ -2639,6 +2652,7 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
 }
 
 const char* packos_last_encoder(void) { return g_last_encoder; }
+
 
 int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uint64_t* offsets, uint64_t stride,
                         size_t n, packos_column* out_cols, uint32_t* status, void* stream) {
@@ -2670,6 +2684,14 @@ int packos_decode_batch(const packos_schema* cs, const uint8_t* arena, const uin
         if (!(scalar && nd.nullable) && nd.kind != K_TUPLE && nd.kind != K_MAP) dc.valid[c] = nullptr;
     }
     hipStream_t st = (hipStream_t)stream;
+    if (s->chain_names) {
+        if (s->ext) hipLaunchKernelGGL(k_decode_chain_names<true>, dim3((unsigned)((n + kBlock - 1) / kBlock)),
+                                       dim3(kBlock), 0, st, arena, offsets, stride, (uint64_t)n, status);
+        else hipLaunchKernelGGL(k_decode_chain_names<false>, dim3((unsigned)((n + kBlock - 1) / kBlock)),
+                                dim3(kBlock), 0, st, arena, offsets, stride, (uint64_t)n, status);
+        HIP_TRY(hipGetLastError());
+        return PACKOS_OK;
+    }
     const int64_t B = s->all_present_size;
     bool fast = s->dec_fast == 1 && ((uintptr_t)arena & 15) == 0 && (offsets || stride == (uint64_t)B) &&
                 !s->tune.decode_generic;

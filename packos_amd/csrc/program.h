@@ -24,6 +24,9 @@ enum : uint32_t {
     CHK_DEFAULT = 32u,   // empty payload decodes as the default literal
     CHK_FAIL = 64u,      // encode check only: fails whenever its container is present
                          // (TupleSchemaNamed names / schemas length mismatch, schema.go:1808-1810)
+    CHK_PANIC = 128u,    // encode check only, last in emission order: every blob that passed the
+                         // checks before it panics (EncodeValueNamed indexing past Schemas once
+                         // it has written them all, schema.go:976-987)
     CHK_RANGE = CHK_MIN | CHK_MAX,
     CHK_STR = CHK_PREFIX | CHK_SUFFIX,
 };

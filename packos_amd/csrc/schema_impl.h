@@ -70,6 +70,12 @@ struct packos_schema {
     std::vector<int> col_node;         // column -> node
     std::vector<packos_column_info> col_info;
     int n_top = 0;
+    // SchemaNamedChain whose len(FieldNames) != len(Schemas): len(FieldNames),
+    // else 0.  EncodeValueNamed walks FieldNames (fewer: only that many fields
+    // are written; more: a panic once the schemas are written), DecodeBufferNamed
+    // fails every blob NewSeqGetAccess accepts (schema.go:948-995); ValidateBuffer
+    // takes the plain SchemaChain (unchanged)
+    int chain_names = 0;
 
     // encode program (host copies)
     std::vector<packos::EncItem> items;

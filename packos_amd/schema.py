@@ -413,7 +413,7 @@ class SchemaChain:
 
         names = getattr(self, "FieldNames", None)
         for t, s in enumerate(self.Schemas):
-            rec(s, 0, t, names[t] if names else "")
+            rec(s, 0, t, names[t] if names and t < len(names) else "")
         return out
 
     def columns(self):

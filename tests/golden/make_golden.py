@@ -162,6 +162,17 @@ ENCODE = [
          TUP(I16, BOOL, {"type": "string", "width": 2}, names=["num", "flag", "lang"])]},
      {"firstTuple": {"year": 2025, "flag": False, "code": S("az")},
       "secondTuple": {"num": 7, "flag": True, "lang": S("go")}}, ("packable/pack_test.go", 134)),
+    # derived (schema.go:968-995): EncodeValueNamed walks FieldNames, so a
+    # SchemaNamedChain with a third schema but two names writes the two named
+    # tuples only -- the same 34 bytes as above
+    ("derived_named_chain_fewer_names", "derived: schema/schema.go:968-995 (expected = packable/pack_test.go:134)",
+     "putaccess",
+     {"type": "chain", "fieldNames": ["firstTuple", "secondTuple"], "schema": [
+         TUP(I32, BOOL, {"type": "string", "width": 2}, names=["year", "flag", "code"]),
+         TUP(I16, BOOL, {"type": "string", "width": 2}, names=["num", "flag", "lang"]),
+         TUP(I16, names=["extra"])]},
+     {"firstTuple": {"year": 2025, "flag": False, "code": S("az")},
+      "secondTuple": {"num": 7, "flag": True, "lang": S("go")}}, ("packable/pack_test.go", 134)),
 ]
 
 # groups whose encodings the reference asserts equal (no literal bytes)
@@ -310,6 +321,17 @@ DECODE = [
     ("derived_named_names_mismatch", "derived: schema/schema.go:1756-1758", "pack_two_tuples34",
      [TUP(I32, BOOL, {"type": "string", "width": 2}),
       TUP(I16, BOOL, {"type": "string", "width": 2}, names=["num", "flag"])], None, (3 | (1 << 8))),
+    # derived (schema.go:948-956): DecodeBufferNamed fails every blob that
+    # NewSeqGetAccess accepts when len(FieldNames) != len(Schemas), with
+    # ErrConstraintViolated at position -1 -- fewer names and more names
+    ("derived_named_chain_fewer_names_decode", "derived: schema/schema.go:948-956", "pack_two_tuples34",
+     {"type": "chain", "fieldNames": ["firstTuple"], "schema": [
+         TUP(I32, BOOL, {"type": "string", "width": 2}), TUP(I16, BOOL, {"type": "string", "width": 2})]},
+     None, 3),
+    ("derived_named_chain_more_names_decode", "derived: schema/schema.go:948-956", "pack_two_tuples34",
+     {"type": "chain", "fieldNames": ["firstTuple", "secondTuple", "third"], "schema": [
+         TUP(I32, BOOL, {"type": "string", "width": 2}), TUP(I16, BOOL, {"type": "string", "width": 2})]},
+     None, 3),
     ("decode_empty_tuples2", "schema/schema_test.go:840-869", "schema_empty_tuples2",
      [I16, TUP(STR, STR, STR), TUP(), TUP(STR, names=["ok"]), TUP(names=[]), I16],
      [5, None, None, None, None, 5], 0),

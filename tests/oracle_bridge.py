@@ -30,7 +30,7 @@ class OrSchema(C.Structure):
     _fields_ = [("nodes", C.c_void_p), ("n_nodes", C.c_int), ("n_top", C.c_int),
                 ("lit", C.c_void_p), ("lit_off", C.c_void_p), ("n_cols", C.c_int),
                 ("col_of_node", C.c_int32 * 512), ("next_sibling", C.c_int32 * 512),
-                ("top_nodes", C.c_int32 * 256), ("ext", C.c_void_p)]
+                ("top_nodes", C.c_int32 * 256), ("ext", C.c_void_p), ("chain_names", C.c_int)]
 
 
 class OrGet(C.Structure):
@@ -167,6 +167,8 @@ class OracleSchema:
         s.n_top = len(chain.Schemas)
         s.lit = _ptr(self.lit)
         s.lit_off = _ptr(self.lit_off)
+        names = getattr(chain, "FieldNames", None)   # SchemaNamedChain
+        s.chain_names = len(names) if names and len(names) != len(chain.Schemas) else 0
         if lib().or_schema_prepare(C.byref(s)) != 0:
             raise ValueError("oracle rejected schema")
         self.s = s

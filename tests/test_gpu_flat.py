@@ -180,8 +180,10 @@ def test_flat_capacity_overrun():
 
 
 @pytest.mark.parametrize("name,cap_scale,flags,want", [
-    ("C5", 1, 0, "flat"), ("C5", 3, 0, "flat"), ("C5", 1, 4, "flat"),
-    ("C3", 1, 0, "tiles"), ("C3", 4, 0, "tiles"),
+    # no exact capacity and >= 256 B per blob of it: both kernels launched,
+    # the device picks (flat for C5's 969-B mean, tiles for C3's 85 B)
+    ("C5", 1, 0, "flat|tiles"), ("C5", 3, 0, "flat|tiles"), ("C5", 1, 4, "flat"),
+    ("C3", 1, 0, "tiles"), ("C3", 4, 0, "flat|tiles"),
     # C3 declared exact: 24 var bytes per blob, a 32-B staging pool, six
     # workgroups per CU (k_encode_tiles<true, 1, 6>)
     ("C3", 1, 4, "tiles6"),
@@ -189,8 +191,10 @@ def test_flat_capacity_overrun():
     ("C3", 4, 4, "flat")])
 def test_flat_auto_dispatch(name, cap_scale, flags, want, monkeypatch):
     """PACKOS_ENC_FLAT unset: the flat / tiles choice follows the batch's mean
-    blob size (static bytes + var bytes read back from the offsets), not the
-    arena the caller passed; PACKOS_ENC_CAP_EXACT (4) takes out_capacity / n."""
+    blob size (static bytes + var bytes), not the arena the caller passed:
+    PACKOS_ENC_CAP_EXACT (4) takes out_capacity / n on the host; without it a
+    capacity of >= 256 B per blob launches both kernels and the device decides
+    (no read-back)."""
     monkeypatch.delenv("PACKOS_ENC_FLAT", raising=False)
     cfg = CONFIGS[name]
     hc = make_columns(cfg, n=3000)
@@ -214,3 +218,71 @@ def test_tiles6_pool_overflow_and_tail(mode, n, monkeypatch):
         rws.append([i - 500, "x" * ln, (i * 7919) - 10 ** 12, "abcdefgh"])
     hc = HostColumns.from_rows(chain, rws)
     check(chain, hc, mode, f"tiles6 n={n} mode {mode}", kernel="tiles6", flags=_lib.ENC_CAP_EXACT)
+
+
+def _graph_replay(T, fn):
+    """fn() captured into a HIP graph on a side stream, replayed twice."""
+    s = T.cuda.Stream()
+    s.wait_stream(T.cuda.current_stream())
+    with T.cuda.stream(s):
+        fn()   # warm-up outside the capture (schema tables, pipelines)
+    T.cuda.current_stream().wait_stream(s)
+    T.cuda.synchronize()
+    g = T.cuda.CUDAGraph()
+    with T.cuda.graph(g):
+        fn()
+    for _ in range(2):
+        g.replay()
+    T.cuda.synchronize()
+
+
+@pytest.mark.parametrize("name", ["C3", "C5"])
+def test_encode_plan_graph_capture_oversized_arena(name, monkeypatch):
+    """EncodePlan.run() with an `out` twice the batch's size, captured in a
+    graph and replayed: no host sync inside the call (a hipStreamSynchronize
+    on a capturing stream would fail the capture), bytes identical to the
+    oracle's."""
+    monkeypatch.delenv("PACKOS_ENC_FLAT", raising=False)
+    from packos_amd.api import EncodePlan
+    T = torch()
+    cfg = CONFIGS[name]
+    hc = make_columns(cfg, n=5000)
+    a0, o0, _ = ob.encode(cfg.chain, hc, cfg.mode, nthreads=8)
+    s = CompiledSchema(cfg.chain, cfg.mode)
+    dc = DeviceColumns.from_host(s, hc, "cuda:0")
+    big = T.zeros(2 * int(o0[hc.n]) + 64, dtype=T.uint8, device="cuda:0")
+    plan = EncodePlan(s, dc, out=big)
+    plan.offsets.fill_(-1)
+    _graph_replay(T, plan.run)
+    assert np.array_equal(plan.offsets.cpu().numpy().astype(np.uint64), o0)
+    assert np.array_equal(big[: int(o0[hc.n])].cpu().numpy(), a0)
+
+
+@pytest.mark.parametrize("name,cap_scale", [("C3", 4), ("C5", 2)])
+def test_device_pick_graph_capture(name, cap_scale, monkeypatch):
+    """packos_encode_batch with neither PACKOS_ENC_CAP_EXACT nor a small
+    capacity: the flat / tiles choice is made on the device (both kernels
+    launched), inside a graph capture, bit-exact against the oracle."""
+    monkeypatch.delenv("PACKOS_ENC_FLAT", raising=False)
+    T = torch()
+    cfg = CONFIGS[name]
+    hc = make_columns(cfg, n=4000)
+    a0, o0, s0 = ob.encode(cfg.chain, hc, 0, nthreads=8)
+    s = CompiledSchema(cfg.chain, 0)
+    dc = DeviceColumns.from_host(s, hc, "cuda:0")
+    arr = dc.ctypes_array()
+    n = hc.n
+    L = _lib.lib()
+    out = T.zeros(int(o0[n]) * cap_scale + 16, dtype=T.uint8, device="cuda:0")
+    offs = T.full((n + 1,), -1, dtype=T.int64, device="cuda:0")
+    st = T.full((n,), -1, dtype=T.int32, device="cuda:0")
+
+    def call():
+        rc = L.packos_encode_batch(s.handle, arr, n, out.data_ptr(), out.numel(), offs.data_ptr(), st.data_ptr(),
+                                   None, 0, 0, T.cuda.current_stream().cuda_stream)
+        assert rc == 0, L.packos_last_error()
+    _graph_replay(T, call)
+    assert L.packos_last_encoder().decode() == "flat|tiles"
+    assert np.array_equal(offs.cpu().numpy().astype(np.uint64), o0)
+    assert np.array_equal(out[: int(o0[n])].cpu().numpy(), a0)
+    assert np.array_equal(st.cpu().numpy().astype(np.uint32), s0)

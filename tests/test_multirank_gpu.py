@@ -102,3 +102,24 @@ def test_bench_two_ranks_rehearsal():
     # ... its WHOLE shard, in 7000-blob pieces (a flag per rank: all pieces, all blobs)
     assert line["parity"]["checked_blobs_per_rank_min"] > 14000
     assert len(line["passes"]["order"]) == 3 and set(line["passes"]["order"]) == {"cold"}
+
+
+def test_bench_gpus_2_launches_its_own_ranks():
+    """`python bench.py --gpus 2` with NO external launcher: bench.py starts the
+    two ranks itself (rehearsal env: both on cuda:0, gloo), and the one line
+    says n_gpus 2 with every rank's whole shard bit-exact."""
+    env = dict(os.environ, PACKOS_BENCH_DEVICE="0", PACKOS_BENCH_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "PACKOS_BENCH_RANK_CHILD"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "C3", "--blobs-per-gpu", "30000",
+           "--steps", "3", "--warmup", "1", "--sets", "1", "--no-host", "--no-warm", "--parity-piece", "8000"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["world_size"] == 2 and line["config"]["backend"] == "gloo"
+    assert [m[0] for m in line["config"]["rank_devices"]] == [0, 1]
+    assert line["config"]["global_blobs"] == 60000 and line["value"] > 0
+    assert line["parity"]["result"] == "bit-exact" and line["parity"]["ranks"] == 2
+    assert line["parity"]["checked_blobs_per_rank_min"] > 25000

@@ -1,0 +1,61 @@
+"""Where do two encoders' bytes differ?  For the random-schema encode cases of
+tests/test_gpu_parity.py (seeds x modes x offsets paths), run the library
+PACKOS_LIB points at and report, per failing case, the kernel that ran, the
+tile-relative position of every differing blob and byte, and which encode
+item (header block / literal / fixed / var) the first differing bytes belong
+to.  Diagnostic only (never a test): compares with the CPU oracle.
+
+    PACKOS_LIB=abl/libpackos_x.so python tools/tiles_diag.py [seeds]
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+
+import oracle_bridge as ob  # noqa: E402
+from packos_amd import _lib  # noqa: E402
+from packos_amd.columns import HostColumns  # noqa: E402
+from schema_gen import rand_chain, rand_rows  # noqa: E402
+from test_gpu_parity import gpu_encode  # noqa: E402
+
+
+def main():
+    seeds = range(int(sys.argv[1])) if len(sys.argv) > 1 else range(60)
+    L = _lib.lib()
+    nfail = 0
+    for seed in seeds:
+        chain = rand_chain(seed)
+        n = 257 + 300 * (seed % 3)
+        hc = HostColumns.from_rows(chain, rand_rows(chain, n, seed * 7 + 1))
+        for mode in (0, 1):
+            for fused in (False, True):
+                a0, o0, s0 = ob.encode(chain, hc, mode, nthreads=8)
+                a1, o1, s1 = gpu_encode(chain, hc, mode, 0, fused)
+                enc = L.packos_last_encoder().decode() if hasattr(L, "packos_last_encoder") else "?"
+                if np.array_equal(a0, a1) and np.array_equal(o0, o1) and np.array_equal(s0, s1):
+                    continue
+                nfail += 1
+                bad = np.nonzero(a0 != a1)[0]
+                blobs = np.unique(np.searchsorted(o0, bad, side="right") - 1)
+                valid = [c for c, v in enumerate(hc.valid) if v is not None]
+                print(f"FAIL seed {seed} mode {mode} fused {fused} n {n} kernel {enc}: {bad.size} bytes in "
+                      f"{blobs.size} blobs; offsets equal {np.array_equal(o0, o1)}, status equal "
+                      f"{np.array_equal(s0, s1)}; validity columns {valid}")
+                print(f"   schema {chain!r}"[:400])
+                tiles = np.unique(blobs // 128)
+                print(f"   tiles {tiles[:20].tolist()} blob-in-tile {sorted(set((blobs % 128).tolist()))[:40]}")
+                for b in blobs[:4]:
+                    lo, hi = int(o0[b]), int(o0[b + 1])
+                    d = np.nonzero(a0[lo:hi] != a1[lo:hi])[0]
+                    print(f"   blob {b} ({hi - lo} B) differs at {d[:16].tolist()}")
+                    print(f"     want {a0[lo:hi][:64].tobytes().hex()}")
+                    print(f"     got  {a1[lo:hi][:64].tobytes().hex()}")
+                sys.stdout.flush()
+    print(f"{nfail} failing cases")
+
+
+if __name__ == "__main__":
+    main()
