@@ -123,6 +123,20 @@ def test_flat_random_flat(seed, flat_on):
     check(chain, hc, seed % 2, f"seed {seed}", shift=seed % 3 == 1, off64=seed % 4 == 3, kernel=flat_on)
 
 
+@pytest.mark.parametrize("slice_bytes", ["0", "64", "700", "4096"])
+@pytest.mark.parametrize("seed", range(0, 40, 3))
+def test_flat_output_slices(seed, slice_bytes, flat_on, monkeypatch):
+    """Tiles written by several workgroups (PACKOS_FLAT_SLICE output bytes
+    each, up to 16 per tile; 0: one per tile): every slice boundary (inside a
+    static run, a var value, between blobs, the ragged last tile), bit-exact."""
+    monkeypatch.setenv("PACKOS_FLAT_SLICE", slice_bytes)
+    rng = random.Random(seed)
+    chain = flat_chain(rng)
+    n = [127, 128, 300, 1000, 2049][seed % 5]
+    hc = HostColumns.from_rows(chain, rows(chain, n, seed * 13 + 1))
+    check(chain, hc, seed % 2, f"seed {seed} slice {slice_bytes}", kernel=flat_on)
+
+
 def test_flat_wide_fixed_leaf_falls_back():
     """A fixed leaf over 16 B is outside k_encode_flat's plan: the tile
     encoder takes the chain, bit-exact."""
@@ -182,8 +196,8 @@ def test_flat_capacity_overrun():
 @pytest.mark.parametrize("name,cap_scale,flags,want", [
     # no exact capacity and >= 256 B per blob of it: both kernels launched,
     # the device picks (flat for C5's 969-B mean, tiles for C3's 85 B)
-    ("C5", 1, 0, "flat|tiles"), ("C5", 3, 0, "flat|tiles"), ("C5", 1, 4, "flat"),
-    ("C3", 1, 0, "tiles"), ("C3", 4, 0, "flat|tiles"),
+    ("C5", 1, 0, ("flat|tiles", "flat|tiles6")), ("C5", 3, 0, ("flat|tiles", "flat|tiles6")), ("C5", 1, 4, "flat"),
+    ("C3", 1, 0, "tiles"), ("C3", 4, 0, ("flat|tiles", "flat|tiles6")),
     # C3 declared exact: 24 var bytes per blob, a 32-B staging pool, six
     # workgroups per CU (k_encode_tiles<true, 1, 6>)
     ("C3", 1, 4, "tiles6"),
@@ -282,7 +296,7 @@ def test_device_pick_graph_capture(name, cap_scale, monkeypatch):
                                    None, 0, 0, T.cuda.current_stream().cuda_stream)
         assert rc == 0, L.packos_last_error()
     _graph_replay(T, call)
-    assert L.packos_last_encoder().decode() == "flat|tiles"
+    assert L.packos_last_encoder().decode() in ("flat|tiles", "flat|tiles6")
     assert np.array_equal(offs.cpu().numpy().astype(np.uint64), o0)
     assert np.array_equal(out[: int(o0[n])].cpu().numpy(), a0)
     assert np.array_equal(st.cpu().numpy().astype(np.uint32), s0)

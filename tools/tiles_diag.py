@@ -23,6 +23,8 @@ from test_gpu_parity import gpu_encode  # noqa: E402
 
 
 def main():
+    import torch
+    torch.cuda.init()   # the HIP runtime up before the library's first call
     seeds = range(int(sys.argv[1])) if len(sys.argv) > 1 else range(60)
     L = _lib.lib()
     nfail = 0
