@@ -123,20 +123,6 @@ def test_flat_random_flat(seed, flat_on):
     check(chain, hc, seed % 2, f"seed {seed}", shift=seed % 3 == 1, off64=seed % 4 == 3, kernel=flat_on)
 
 
-@pytest.mark.parametrize("slice_bytes", ["0", "64", "700", "4096"])
-@pytest.mark.parametrize("seed", range(0, 40, 3))
-def test_flat_output_slices(seed, slice_bytes, flat_on, monkeypatch):
-    """Tiles written by several workgroups (PACKOS_FLAT_SLICE output bytes
-    each, up to 16 per tile; 0: one per tile): every slice boundary (inside a
-    static run, a var value, between blobs, the ragged last tile), bit-exact."""
-    monkeypatch.setenv("PACKOS_FLAT_SLICE", slice_bytes)
-    rng = random.Random(seed)
-    chain = flat_chain(rng)
-    n = [127, 128, 300, 1000, 2049][seed % 5]
-    hc = HostColumns.from_rows(chain, rows(chain, n, seed * 13 + 1))
-    check(chain, hc, seed % 2, f"seed {seed} slice {slice_bytes}", kernel=flat_on)
-
-
 def test_flat_wide_fixed_leaf_falls_back():
     """A fixed leaf over 16 B is outside k_encode_flat's plan: the tile
     encoder takes the chain, bit-exact."""
