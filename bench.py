@@ -828,8 +828,8 @@ def main():
         dist.all_reduce(mins, op=dist.ReduceOp.MIN)
         parity = {"result": "bit-exact" if int(mins[0].item()) == 1 else "MISMATCH", "ranks": world,
                   "blobs_rank0": n, "checked_blobs_per_rank_min": int(mins[1].item()), "sha256_16_rank0": digest,
-                  "checked": "every rank: its whole GPU shard (in 1M-blob pieces) vs the CPU oracle's encoding of "
-                             "the same global slice"}
+                  "checked": f"every rank: its whole GPU shard (in {max(1, args.parity_piece)}-blob pieces) vs the CPU "
+                             "oracle's encoding of the same global slice"}
     if args.op != "encode" and os.environ.get("PACKOS_BENCH_NO_PARITY") is None:
         # the timed run's set-0 outputs vs the CPU oracle over this rank's whole
         # shard (every rank; flags meet in a MIN)

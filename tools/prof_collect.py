@@ -99,7 +99,8 @@ def main():
             pc = one(os.path.join(src, f"{tag}_{pass_}", "**", "*counter_collection.csv"))
             if not pc or not kname:
                 continue
-            shutil.copy(pc, os.path.join(dst, f"{tag}_pmc_{pass_.lower()}.csv"))
+            if pass_ != "SQ":   # the SQ pass is kept as its per-wave summary in <tag>.json only
+                shutil.copy(pc, os.path.join(dst, f"{tag}_pmc_{pass_.lower()}.csv"))
             med, cnt = per_launch(pc, kname)
             if pass_ == "FETCH_SIZE" and "FETCH_SIZE" in med:
                 raw = med["FETCH_SIZE"] * 1024
