@@ -29,14 +29,19 @@ def torch():
     return t
 
 
-def gpu_encode(chain, hc, mode=0, flags=0, fused=False):
+def gpu_encode(chain, hc, mode=0, flags=0, fused=False, poison=False):
     """fused=True: size the arena with the size pass, then encode WITHOUT
     PACKOS_ENC_OFFSETS_READY into poisoned offsets, so the single-pass kernel's
-    own sizes + look-back scan must produce them."""
+    own sizes + look-back scan must produce them.  poison: the arena starts
+    filled with 0xCD (bytes an encoder never stores stay visible)."""
     T = torch()
     s = CompiledSchema(chain, mode)
     dc = DeviceColumns.from_host(s, hc, "cuda:0")
-    r = encode_batch(s, dc, flags=flags)
+    out = None
+    if poison:
+        a0, o0, _ = ob.encode(chain, hc, mode, nthreads=8)
+        out = T.full((max(int(o0[hc.n]), 16),), 0xCD, dtype=T.uint8, device="cuda:0")
+    r = encode_batch(s, dc, flags=flags, out=out)
     if fused and r.blob_size < 0 and hc.n:
         L = _lib.lib()
         n = hc.n

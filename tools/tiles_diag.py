@@ -35,7 +35,7 @@ def main():
         for mode in (0, 1):
             for fused in (False, True):
                 a0, o0, s0 = ob.encode(chain, hc, mode, nthreads=8)
-                a1, o1, s1 = gpu_encode(chain, hc, mode, 0, fused)
+                a1, o1, s1 = gpu_encode(chain, hc, mode, 0, fused, poison=True)
                 enc = L.packos_last_encoder().decode() if hasattr(L, "packos_last_encoder") else "?"
                 if np.array_equal(a0, a1) and np.array_equal(o0, o1) and np.array_equal(s0, s1):
                     continue
@@ -49,7 +49,25 @@ def main():
                 print(f"   schema {chain!r}"[:400])
                 tiles = np.unique(blobs // 128)
                 print(f"   tiles {tiles[:20].tolist()} blob-in-tile {sorted(set((blobs % 128).tolist()))[:40]}")
-                for b in blobs[:4]:
+                # runs of differing bytes: tile, offset from the tile's 16-B chunk
+                # origin, and what was there (cd: never stored, 00: zero stored)
+                runs, st_ = [], None
+                for x in bad.tolist() + [None]:
+                    if st_ is not None and (x is None or x != pv + 1):
+                        runs.append((st_, pv + 1))
+                        st_ = None
+                    if x is not None and st_ is None:
+                        st_ = x
+                    pv = x
+                for r0_, r1_ in runs[:8]:
+                    bl = int(np.searchsorted(o0, r0_, side="right") - 1)
+                    t = bl // 128
+                    ga = int(o0[128 * t]) & ~15
+                    got = a1[r0_:r1_]
+                    kind = "cd" if (got == 0xCD).all() else "00" if (got == 0).all() else "mixed"
+                    print(f"   run [{r0_},{r1_}) len {r1_ - r0_} tile {t} rel-ga [{r0_ - ga},{r1_ - ga}) "
+                          f"chunks {(r0_ - ga) >> 4}..{(r1_ - 1 - ga) >> 4} got {kind}")
+                for b in blobs[:2]:
                     lo, hi = int(o0[b]), int(o0[b + 1])
                     d = np.nonzero(a0[lo:hi] != a1[lo:hi])[0]
                     print(f"   blob {b} ({hi - lo} B) differs at {d[:16].tolist()}")
