@@ -59,6 +59,15 @@ def main():
                     if x is not None and st_ is None:
                         st_ = x
                     pv = x
+                spans = []   # top-level item spans (GetAccess GET_SPAN): which item a run lies in
+                for k in range(len(chain.Schemas)):
+                    _, _, _, tg, _ = ob.get_batch(a0, o0, n, [k], 2, values=False)
+                    ss, sl, sst = np.zeros(n, np.int64), np.zeros(n, np.int64), np.ones(n, np.uint8)
+                    for t_ in np.unique(tg):
+                        _, s_, l_, _, st_2 = ob.get_batch(a0, o0, n, [k], 2, int(t_), -1, values=False)
+                        m_ = (tg == t_) & (st_2 == 0)
+                        ss[m_], sl[m_], sst[m_] = s_[m_], l_[m_], 0
+                    spans.append((ss, sl, sst))
                 for r0_, r1_ in runs[:8]:
                     bl = int(np.searchsorted(o0, r0_, side="right") - 1)
                     t = bl // 128
@@ -66,7 +75,19 @@ def main():
                     got = a1[r0_:r1_]
                     kind = "cd" if (got == 0xCD).all() else "00" if (got == 0).all() else "mixed"
                     print(f"   run [{r0_},{r1_}) len {r1_ - r0_} tile {t} rel-ga [{r0_ - ga},{r1_ - ga}) "
-                          f"chunks {(r0_ - ga) >> 4}..{(r1_ - 1 - ga) >> 4} got {kind}")
+                          f"chunks {(r0_ - ga) >> 4}..{(r1_ - 1 - ga) >> 4} got {kind} "
+                          f"blob {bl} [{int(o0[bl])},{int(o0[bl + 1])}) items " + ",".join(
+                              f"{k}:{chain.Schemas[k].kind}{'v' if chain.Schemas[k].variable else ''}[{int(ss[bl])},{int(ss[bl] + sl[bl])})"
+                              for k, (ss, sl, sst) in enumerate(spans)
+                              if sst[bl] == 0 and ss[bl] < r1_ and ss[bl] + sl[bl] > r0_))
+                # tile 0's never-stored 16-B chunks as (wave, chunk step m, lane):
+                # chunk c of a tile belongs to wave (c / 64) % 4, step c / 256, lane c % 64
+                t0e = int(o0[min(128, n)])
+                miss = sorted({(x >> 4) for x in bad.tolist() if x < t0e and a1[x] == 0xCD})
+                print(f"   tile 0: {len(miss)} of {(t0e + 15) >> 4} chunks never stored; by (wave, m): " + "; ".join(
+                    f"w{w} m{m}: lanes " + ",".join(str(c % 64) for c in miss if (c // 64) % 4 == w and c // 256 == m)
+                    for m in range(4) for w in range(4)
+                    if any((c // 64) % 4 == w and c // 256 == m for c in miss)))
                 for b in blobs[:2]:
                     lo, hi = int(o0[b]), int(o0[b + 1])
                     d = np.nonzero(a0[lo:hi] != a1[lo:hi])[0]
