@@ -874,7 +874,10 @@ namespace packos {
 void set_error(const std::string& m) { g_err = m; }
 
 void read_tune(Tune& t) {
-    if (const char* e = getenv("PACKOS_VAR_PER")) t.var_per = std::max(0, std::min(256, atoi(e)));
+    if (const char* e = getenv("PACKOS_VAR_PER")) {
+        t.var_per = std::max(0, std::min(256, atoi(e)));
+        t.var_per_set = true;
+    }
     t.sizes_scan = getenv("PACKOS_SIZES_SCAN") != nullptr;
     t.decode_generic = getenv("PACKOS_DECODE_GENERIC") != nullptr;
     if (const char* e = getenv("PACKOS_DEC_TILE_BYTES")) t.dec_tile_bytes = std::min(49152, std::max(1024, atoi(e)));

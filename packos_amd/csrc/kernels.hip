@@ -2574,6 +2574,21 @@ static int encode_batch_impl(packos_schema* s, DeviceTables* t, const EncCols& e
             }
         }
     }
+    // closed form, exact capacity: when the batch's var bytes per blob (mean m)
+    // overflow the default staging pool, a pool of 1.1 m + 4 B per blob (a
+    // tile's mean varies around m; 8-B steps, <= kVPoolMax) — unstaged values
+    // are holes, which cost twice as much (labels of 8..110 B: 0.136 -> 0.072
+    // ms; a larger pool at the same LDS occupancy estimate measured slower at
+    // small m: profiles/r06/var_pool_ab.txt)
+    if (planned && !six && V.aff && affine && (flags & PACKOS_ENC_CAP_EXACT) && n && !s->tune.var_per_set &&
+        cap >= (uint64_t)A.C * n) {
+        const uint64_t m = (cap - (uint64_t)A.C * n) / n;
+        const uint64_t per = (m * 11 / 10 + 4 + 7) & ~(uint64_t)7;
+        VPlan Vb;
+        if (per > (uint64_t)s->tune.var_per && per <= kVPoolMax && var_plan(s, ec, !affine, Vb, (uint32_t)per) &&
+            Vb.aff)
+            V = Vb;
+    }
     V.pick = pick ? 2u : 0u;
     V.pick_C = A.C;
     if (planned) {

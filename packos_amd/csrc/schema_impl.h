@@ -45,6 +45,7 @@ struct Node {
 // when the output capacity averages >= 256 B per blob).
 struct Tune {
     int var_per = 40;
+    bool var_per_set = false;    // PACKOS_VAR_PER given: no data-sized pool
     bool sizes_scan = false;
     bool decode_generic = false;
     int dec_tile_bytes = 0;      // 0: 24 KB for B >= 128, else 16 KB
