@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <numeric>
+#include <type_traits>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -277,15 +278,19 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_tile(FixProgram P, FixS
     const uint32_t b0s = contig ? (s / G) * PER * G + s % G : s;   // this thread's first blob
     uint32_t a = (uint32_t)sg.a + b0s * sg.w;   // LDS byte address of this thread's first dword
     const uint32_t xs = (contig ? G : R) * sg.w, xm = sg.mask;
-    const uint32_t nxi = T * (uint32_t)P.nx;
-    DwDesc xd;  // this thread's first X item
-    if (tid < nxi) xd = P.xdw[tid % (uint32_t)P.nx];
+    // X items i = blob * nx + x, taken at a stride SX that is a multiple of nx
+    // (the largest <= the block), so a thread keeps ONE descriptor for all its
+    // items, loaded here with the DMAs in flight (a stride of the block size
+    // reloaded a descriptor from global memory per item: C2 has 768 X items)
+    const uint32_t nx = (uint32_t)P.nx, nxi = T * nx, SX = nx ? (kBlock / nx) * nx : 0u;
+    DwDesc xd;  // this thread's X descriptor
+    if (tid < nxi && tid < SX) xd = P.xdw[tid % nx];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     uint32_t* l32 = (uint32_t*)lds;
     if (nxi) {
         auto assemble = [&](uint32_t i, const DwDesc& d) {
-            const uint32_t j = i / (uint32_t)P.nx;
+            const uint32_t j = i / nx;
             uint32_t val = 0;
 #pragma unroll
             for (int g = 0; g < 4; g++) {
@@ -297,8 +302,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_fixed_tile(FixProgram P, FixS
             }
             l32[((uint32_t)P.x_lds >> 2) + i] = val;
         };
-        if (tid < nxi) assemble(tid, xd);
-        for (uint32_t i = tid + kBlock; i < nxi; i += kBlock) assemble(i, P.xdw[i % (uint32_t)P.nx]);
+        if (tid < SX)
+            for (uint32_t i = tid; i < nxi; i += SX) assemble(i, xd);
         __syncthreads();
     }
     if (s < R) {  // R * Q4 <= 256: the rest of the threads idle here
@@ -1447,12 +1452,25 @@ __device__ __forceinline__ void dfix_tile(const DecFixProgram& F, const DecCols&
                     __builtin_nontemporal_store(dfix_unit(lds, kind, 64u * blk + lane, w, off, magic, SB),
                                                 (g_v4*)dst + lane);
             } else {
+                // the step's kind is wave-uniform: one branch per step, then four
+                // dwords of a compile-time kind (no switch per dword)
+                auto dwords = [&](auto kc) {
+                    constexpr uint32_t KC = decltype(kc)::value;
 #pragma unroll
-                for (uint32_t k = 0; k < 4; k++) {
-                    const uint32_t dl = lane + 64u * k;
-                    if (dl < nd)
-                        __builtin_nontemporal_store(dfix_dword(lds, kind, 256u * blk + dl, w, off, magic, SB),
-                                                    (uint32_t*)dst + dl);
+                    for (uint32_t k = 0; k < 4; k++) {
+                        const uint32_t dl = lane + 64u * k;
+                        if (dl < nd)
+                            __builtin_nontemporal_store(dfix_dword<KC>(lds, kind, 256u * blk + dl, w, off, magic, SB),
+                                                        (uint32_t*)dst + dl);
+                    }
+                };
+                switch (kind) {
+                    case DS_D4: dwords(std::integral_constant<uint32_t, DS_D4>{}); break;
+                    case DS_D2: dwords(std::integral_constant<uint32_t, DS_D2>{}); break;
+                    case DS_D1: dwords(std::integral_constant<uint32_t, DS_D1>{}); break;
+                    case DS_BOOL: dwords(std::integral_constant<uint32_t, DS_BOOL>{}); break;
+                    case DS_GEN: dwords(std::integral_constant<uint32_t, DS_GEN>{}); break;
+                    default: dwords(std::integral_constant<uint32_t, DS_ANY>{}); break;
                 }
             }
         }
