@@ -27,6 +27,10 @@ def main():
     torch.cuda.init()   # the HIP runtime up before the library's first call
     seeds = range(int(sys.argv[1])) if len(sys.argv) > 1 else range(60)
     L = _lib.lib()
+    dbg = hasattr(L, "packos_dbg_read")
+    if dbg:
+        import ctypes
+        L.packos_dbg_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     nfail = 0
     for seed in seeds:
         chain = rand_chain(seed)
@@ -35,6 +39,8 @@ def main():
         for mode in (0, 1):
             for fused in (False, True):
                 a0, o0, s0 = ob.encode(chain, hc, mode, nthreads=8)
+                if dbg:   # probe build (tools/patches/tiles_probe.py dbg): clear its tables
+                    L.packos_dbg_read(None, None, 1)
                 a1, o1, s1 = gpu_encode(chain, hc, mode, 0, fused, poison=True)
                 enc = L.packos_last_encoder().decode() if hasattr(L, "packos_last_encoder") else "?"
                 if np.array_equal(a0, a1) and np.array_equal(o0, o1) and np.array_equal(s0, s1):
@@ -88,6 +94,19 @@ def main():
                     f"w{w} m{m}: lanes " + ",".join(str(c % 64) for c in miss if (c // 64) % 4 == w and c // 256 == m)
                     for m in range(4) for w in range(4)
                     if any((c // 64) % 4 == w and c // 256 == m for c in miss)))
+                if dbg:
+                    D = np.zeros(4096 * 8, np.uint64)
+                    K = np.zeros(4096 * 2048, np.uint8)
+                    L.packos_dbg_read(D.ctypes.data, K.ctypes.data, 0)
+                    print(f"   tile 0 probe: HT {D[0]} NC {D[1]} ne {D[2]} org {D[3]} erel {D[4]} ga {D[5]} "
+                          f"o_end {D[6]} written {D[7]}")
+                    kc = K[:2048]
+                    nc = int(D[1])
+                    print("   tile 0 chunk kinds (0 none, 1 hole, 2 image, 3 edge listed, 7 edge stored): all " +
+                          str({int(v): int((kc[:nc] == v).sum()) for v in np.unique(kc[:nc])}) +
+                          "; never-stored " + str({int(v): sum(1 for c in miss if kc[c] == v) for v in
+                                                   np.unique([kc[c] for c in miss])} if miss else {}))
+                    print("   never-stored chunk: kind " + " ".join(f"{c}:{kc[c]}" for c in miss[:40]))
                 for b in blobs[:2]:
                     lo, hi = int(o0[b]), int(o0[b + 1])
                     d = np.nonzero(a0[lo:hi] != a1[lo:hi])[0]
