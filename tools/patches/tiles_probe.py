@@ -36,8 +36,13 @@ if "dbg" in opts:
 __device__ unsigned long long g_tdbg[4096 * 8];
 __device__ unsigned char g_tkind[4096 * 2048];
 """)
-    sub("""                    edges[atomicAdd(ne_cnt, 1u)] = c;""",
-        """                    edges[atomicAdd(ne_cnt, 1u)] = c;
+    if "            if (valid && !in_hole && !in_img) edges[atomicAdd(ne_cnt, 1u)] = c;" in s:   # round-6 form
+        sub("""            if (valid && !in_hole && !in_img) edges[atomicAdd(ne_cnt, 1u)] = c;""",
+            """            if (valid && !in_hole && !in_img) edges[atomicAdd(ne_cnt, 1u)] = c;
+            if (valid && !in_hole && !in_img && blockIdx.x < 4096 && c < 2048) g_tkind[blockIdx.x * 2048 + c] = 3;""")
+    else:
+        sub("""                    edges[atomicAdd(ne_cnt, 1u)] = c;""",
+            """                    edges[atomicAdd(ne_cnt, 1u)] = c;
                     if (blockIdx.x < 4096 && c < 2048) g_tkind[blockIdx.x * 2048 + c] = 3;""")
     sub("""            if (kind[m] == 1) store_chunk(out, ga, 16u * c, org, erel, a0[m]);""",
         """            if (blockIdx.x < 4096 && c < 2048 && kind[m]) g_tkind[blockIdx.x * 2048 + c] = (unsigned char)kind[m];
