@@ -1,8 +1,9 @@
 # Experiment builds only (refactor investigation): applied to a
 # COPY of packos_amd/csrc by tools/abl_build.sh-style scripts, never to the
-# product.  Usage: python tiles_probe.py <csrc copy> [planptr] [dbg]
+# product.  Usage: python tiles_probe.py <csrc copy> [planptr] [flatptr] [dbg]
 #   planptr: k_encode_tiles reads its plan through an opaque pointer to the
 #            kernel-argument segment (same values, different load placement)
+#   flatptr: the same for k_encode_flat's plan
 #   dbg:     per-tile layout values and per-chunk classification of the
 #            non-closed-form chunk passes into device globals, read back by
 #            packos_dbg_read() (tools/tiles_diag.py --dbg)
@@ -30,6 +31,21 @@ if "planptr" in opts:
     asm volatile("" : "+s"(vp4));
     const VPlan& V = *(const VPlan*)vp4;
 #else""")
+if "flatptr" in opts:   # the same perturbation of k_encode_flat (encode_flat.inc)
+    q = d + "/encode_flat.inc"
+    f = open(q).read()
+    old = """void k_encode_flat(FPlan F, uint64_t* __restrict__ offs, uint8_t* __restrict__ out,
+                                                      uint64_t cap, uint64_t n, uint32_t* __restrict__ status) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];"""
+    assert old in f, "flat signature"
+    f = f.replace(old, """void k_encode_flat(FPlan F_, uint64_t* __restrict__ offs, uint8_t* __restrict__ out,
+                                                      uint64_t cap, uint64_t n, uint32_t* __restrict__ status) {
+    typedef __attribute__((address_space(4))) const FPlan c_fplan;
+    c_fplan* fp4 = (c_fplan*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(fp4));
+    const FPlan& F = *(const FPlan*)fp4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];""")
+    open(q, "w").write(f)
 if "dbg" in opts:
     sub("""// k_encode_tiles helpers
 """, """// k_encode_tiles helpers
